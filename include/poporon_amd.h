@@ -1,0 +1,107 @@
+/*
+ * poporon_amd.h -- batch extension of the poporon C API for MI355X.
+ *
+ * The reference has no batch API: callers loop poporon_encode/poporon_decode
+ * one codeword at a time (include/poporon.h:90-91, src/encode.c:236-252,
+ * src/decode.c:596-612).  These entry points take many codewords at once
+ * behind the same handle.  Each per-codeword result equals what the
+ * single-codeword call would return for that codeword (bytes, bool and
+ * corrected_num), see tests/test_gpu_parity.py.
+ *
+ * Layout: codeword c's message is data[c*data_stride .. +size), its parity
+ * parity[c*parity_stride .. +num_roots).  Strides and base pointers may have
+ * any alignment; 4-byte aligned strides/bases take the fast load path.
+ *
+ * Device variants take device pointers (hipMalloc'd or any HIP-visible
+ * allocation, e.g. a torch tensor's data_ptr()) and enqueue asynchronously on
+ * `stream` (a hipStream_t; NULL = the null stream).  Host variants copy
+ * through pinned staging in chunks and return when the results are in host
+ * memory.  A handle is not reentrant (same rule as the reference handle).
+ *
+ * Every entry point returns false and records a message (poporon_amd_last_error)
+ * on invalid arguments, an unsupported configuration, or a HIP failure.  There
+ * is no CPU fallback: without a usable GPU these calls fail.
+ */
+#ifndef POPORON_AMD_H
+#define POPORON_AMD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#include "poporon.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Message for the last failing call on this thread ("" if none). */
+const char *poporon_amd_last_error(void);
+
+/* Number of HIP devices visible (0 when no GPU / no runtime). */
+int poporon_amd_device_count(void);
+
+/* Bind the handle to HIP device `device` (default: the device current at the
+ * handle's first GPU call).  Must be called before any GPU work. */
+bool poporon_amd_set_device(poporon_t *pprn, int device);
+
+/* Pre-size the handle's device workspace for batches of up to max_count
+ * codewords, so that later device calls allocate nothing (graph capture). */
+bool poporon_amd_reserve(poporon_t *pprn, size_t max_count);
+
+/* True when the handle's parameters are served by the GPU kernels
+ * (symbol_size 8, num_roots 32, generator without zero coefficients,
+ * (fcr+num_roots-1)*prim+254 < 65536); false otherwise. */
+bool poporon_amd_supported(const poporon_t *pprn);
+
+/* ---- device-resident batches (asynchronous on `stream`) ------------------ */
+
+bool poporon_encode_batch_device(poporon_t *pprn, const uint8_t *d_data, size_t data_stride, uint8_t *d_parity,
+                                 size_t parity_stride, size_t size, size_t count, void *stream);
+
+/*
+ * Decode in place.  d_positions == NULL: errors-only decode (the handle's
+ * erasure object and external syndromes, if configured, are NOT used by the
+ * batch calls).  Otherwise erasure decode: codeword c's erasure list is
+ * d_positions[c*positions_stride .. +32] (uint8 positions into data[], slots
+ * past the count are read exactly as the reference reads its erasure object,
+ * quirks Q2/Q3), d_counts[c] its count (<= num_roots).
+ * d_ok[c] = decode result (1/0); d_corrected[c] = corrected_num (may be NULL).
+ */
+bool poporon_decode_batch_device(poporon_t *pprn, uint8_t *d_data, size_t data_stride, uint8_t *d_parity,
+                                 size_t parity_stride, size_t size, size_t count, const uint8_t *d_positions,
+                                 size_t positions_stride, const uint8_t *d_counts, uint8_t *d_ok,
+                                 uint8_t *d_corrected, void *stream);
+
+/* Screening without correction: d_dirty[c] = 1 when codeword c has a nonzero
+ * syndrome (the reference's calculate_syndrome_u8 flag, src/decode.c:409-414),
+ * else 0.  Reads data and parity only. */
+bool poporon_check_batch_device(poporon_t *pprn, const uint8_t *d_data, size_t data_stride, const uint8_t *d_parity,
+                                size_t parity_stride, size_t size, size_t count, uint8_t *d_dirty, void *stream);
+
+/* ---- host-memory batches (synchronous) ------------------------------------ */
+
+bool poporon_encode_batch(poporon_t *pprn, const uint8_t *data, size_t data_stride, uint8_t *parity,
+                          size_t parity_stride, size_t size, size_t count);
+
+bool poporon_decode_batch(poporon_t *pprn, uint8_t *data, size_t data_stride, uint8_t *parity, size_t parity_stride,
+                          size_t size, size_t count, const uint8_t *positions, size_t positions_stride,
+                          const uint8_t *counts, uint8_t *ok, uint8_t *corrected);
+
+/* ---- in-library kernel timing ----------------------------------------------
+ * When enabled, every kernel the handle launches is bracketed by HIP events
+ * recorded on the stream it runs on.  poporon_amd_timing(pprn, 1) enables and
+ * resets the totals; poporon_amd_timing_read waits for the recorded events and
+ * returns the summed kernel time (ms) and launch count for one kernel id:
+ * 0 = encode LFSR, 1 = remainder LFSR, 2 = correction, 3 = check LFSR. */
+#define POPORON_AMD_KERNEL_ENCODE 0
+#define POPORON_AMD_KERNEL_REMAINDER 1
+#define POPORON_AMD_KERNEL_CORRECT 2
+#define POPORON_AMD_KERNEL_CHECK 3
+bool poporon_amd_timing(poporon_t *pprn, int enable);
+bool poporon_amd_timing_read(poporon_t *pprn, int kernel, double *total_ms, uint64_t *launches);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* POPORON_AMD_H */

@@ -1,0 +1,1028 @@
+/*
+ * api.cpp -- the poporon C API of libpoporon_amd (include/poporon.h,
+ * include/poporon/erasure.h, include/poporon/gf.h, include/poporon_amd.h).
+ *
+ * Host side of the drop-in boundary.  Object lifetimes and argument rules
+ * follow the reference:
+ *   config objects         src/poporon.c:214-233, :281-284, :301-304
+ *   handle create/destroy  src/poporon.c:57-110, :172-212
+ *   getters, version       src/poporon.c:306-373
+ *   erasure list           src/erasure.c:12-127
+ *   GF handle              src/gf.c:12-91
+ *   generator polynomial   src/rs.c:29-82
+ *   encode/decode checks   src/encode.c:236-252, src/decode.c:418-429, :596-612
+ * All RS arithmetic on codewords runs in the HIP kernels (rs_kernels.hip);
+ * there is no CPU codec in this library.
+ */
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "poporon.h"
+#include "poporon_amd.h"
+#include "rs_device.h"
+
+#ifndef POPORON_BUILDTIME
+#define POPORON_BUILDTIME 1
+#endif
+#define POPORON_VERSION_ID 20000000
+
+#define EXPORT extern "C" __attribute__((visibility("default")))
+
+/* ------------------------------------------------------------------------ */
+/* error reporting                                                          */
+/* ------------------------------------------------------------------------ */
+
+static thread_local std::string g_last_error;
+
+static bool fail(const char *fmt, ...) __attribute__((format(printf, 1, 2)));
+static bool fail(const char *fmt, ...)
+{
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    g_last_error = buf;
+    return false;
+}
+
+#define HIP_OK(expr)                                                                                                  \
+    do {                                                                                                              \
+        hipError_t e_ = (expr);                                                                                       \
+        if (e_ != hipSuccess)                                                                                         \
+            return fail("%s failed: %s", #expr, hipGetErrorString(e_));                                               \
+    } while (0)
+
+EXPORT const char *poporon_amd_last_error(void) { return g_last_error.c_str(); }
+
+/* ------------------------------------------------------------------------ */
+/* objects                                                                  */
+/* ------------------------------------------------------------------------ */
+
+struct _poporon_erasure_t {
+    uint32_t capacity;
+    uint32_t erasure_count;
+    uint32_t *erasure_positions;
+    uint16_t *corrections; /* never written; kept for layout/ownership parity */
+};
+
+struct _poporon_gf_t {
+    uint8_t symbol_size;
+    uint8_t field_size; /* uint8 like the reference struct (src/internal/common.h:46-52) */
+    uint16_t *log2exp;
+    uint16_t *exp2log;
+    uint16_t generator_polynomial;
+};
+
+struct poporon_rs_t {
+    poporon_gf_t *gf;
+    uint16_t first_consecutive_root;
+    uint16_t primitive_element;
+    uint16_t num_roots;
+    uint16_t *generator_polynomial; /* log form */
+};
+
+struct _poporon_config_t {
+    poporon_fec_type_t fec_type;
+    uint8_t symbol_size;
+    uint16_t generator_polynomial;
+    uint16_t first_consecutive_root;
+    uint16_t primitive_element;
+    uint8_t num_roots;
+    poporon_erasure_t *erasure;
+    uint16_t *syndrome;
+};
+
+#define NKERN 4
+struct TimedLaunch {
+    int kernel;
+    hipEvent_t a, b;
+};
+
+struct GpuCtx {
+    bool timing = false;
+    std::vector<TimedLaunch> pending;
+    std::vector<hipEvent_t> event_pool;
+    double total_ms[NKERN] = {0, 0, 0, 0};
+    uint64_t launches[NKERN] = {0, 0, 0, 0};
+    bool ready = false;
+    int device = -1;
+    int num_cu = 256;
+    hipStream_t stream = nullptr;
+    RsDevTables *tab = nullptr; /* device */
+    uint8_t *rem = nullptr;     /* device workspace: 32 B per codeword */
+    size_t rem_cap = 0;
+    /* single-codeword / host-batch staging (device) */
+    uint8_t *stage = nullptr;
+    size_t stage_cap = 0;
+};
+
+struct _poporon_t {
+    poporon_fec_type_t fec_type;
+    poporon_rs_t *rs;
+    uint16_t primitive_inverse;
+    poporon_erasure_t *erasure; /* borrowed, read live at every decode */
+    uint16_t *ext_syndrome;     /* borrowed, read live at every decode */
+    size_t last_corrected;
+    bool supported;
+    RsDevTables host_tab;
+    RsCorrParams corr;
+    GpuCtx gpu;
+};
+
+/* ------------------------------------------------------------------------ */
+/* GF(2^m) and generator (host setup)                                       */
+/* ------------------------------------------------------------------------ */
+
+static inline uint8_t gf_mod(const poporon_gf_t *gf, uint16_t v)
+{
+    while (v >= gf->field_size) {
+        v = (uint16_t)(v - gf->field_size);
+        v = (uint16_t)((v >> gf->symbol_size) + (v & gf->field_size));
+    }
+    return (uint8_t)v;
+}
+
+EXPORT void poporon_gf_destroy(poporon_gf_t *gf)
+{
+    if (!gf)
+        return;
+    free(gf->log2exp);
+    free(gf->exp2log);
+    free(gf);
+}
+
+EXPORT poporon_gf_t *poporon_gf_create(uint8_t symbol_size, uint16_t generator_polynomial)
+{
+    if (symbol_size < 1 || symbol_size > 16)
+        return nullptr;
+    poporon_gf_t *gf = (poporon_gf_t *)calloc(1, sizeof(poporon_gf_t));
+    if (!gf)
+        return nullptr;
+    gf->symbol_size = symbol_size;
+    gf->field_size = (uint8_t)((1u << symbol_size) - 1u);
+    gf->generator_polynomial = generator_polynomial;
+    gf->log2exp = (uint16_t *)calloc((size_t)gf->field_size + 1, sizeof(uint16_t));
+    gf->exp2log = (uint16_t *)calloc((size_t)gf->field_size + 1, sizeof(uint16_t));
+    if (!gf->log2exp || !gf->exp2log) {
+        poporon_gf_destroy(gf);
+        return nullptr;
+    }
+    /* powers of x reduced by the field polynomial; log(0) = field_size */
+    gf->exp2log[0] = gf->field_size;
+    gf->log2exp[gf->field_size] = 0;
+    uint16_t x = 1;
+    for (uint8_t i = 0; i < gf->field_size; i++) {
+        gf->exp2log[x] = i;
+        gf->log2exp[i] = x;
+        x = (uint16_t)(x << 1);
+        if (x & (1u << symbol_size))
+            x ^= generator_polynomial;
+        x &= gf->field_size;
+    }
+    if (x != gf->log2exp[0]) { /* not primitive: the walk did not close */
+        poporon_gf_destroy(gf);
+        return nullptr;
+    }
+    return gf;
+}
+
+EXPORT uint8_t poporon_gf_mod(poporon_gf_t *gf, uint16_t value) { return gf ? gf_mod(gf, value) : 0; }
+
+EXPORT void poporon_rs_destroy(poporon_rs_t *rs)
+{
+    if (!rs)
+        return;
+    poporon_gf_destroy(rs->gf);
+    free(rs->generator_polynomial);
+    free(rs);
+}
+
+/* g(x) = prod_{i<num_roots} (x - alpha^(prim*(fcr+i))), stored in log form.
+ * The root exponent is a uint16 accumulator as in the reference. */
+EXPORT poporon_rs_t *poporon_rs_create(uint8_t symbol_size, uint16_t generator_polynomial,
+                                       uint16_t first_consecutive_root, uint16_t primitive_element, uint8_t num_roots)
+{
+    poporon_gf_t *gf = poporon_gf_create(symbol_size, generator_polynomial);
+    if (!gf)
+        return nullptr;
+    poporon_rs_t *rs = (poporon_rs_t *)calloc(1, sizeof(poporon_rs_t));
+    if (!rs) {
+        poporon_gf_destroy(gf);
+        return nullptr;
+    }
+    rs->gf = gf;
+    rs->first_consecutive_root = first_consecutive_root;
+    rs->primitive_element = primitive_element;
+    rs->num_roots = num_roots;
+    rs->generator_polynomial = (uint16_t *)calloc((size_t)num_roots + 1, sizeof(uint16_t));
+    if (!rs->generator_polynomial) {
+        poporon_rs_destroy(rs);
+        return nullptr;
+    }
+    uint16_t *g = rs->generator_polynomial;
+    g[0] = 1;
+    uint16_t root = (uint16_t)(first_consecutive_root * primitive_element);
+    for (uint16_t i = 0; i < num_roots; i++, root = (uint16_t)(root + primitive_element)) {
+        g[i + 1] = 1;
+        for (uint16_t j = i; j > 0; j--)
+            g[j] = g[j] ? (uint16_t)(g[j - 1] ^ gf->log2exp[gf_mod(gf, (uint16_t)(gf->exp2log[g[j]] + root))])
+                        : g[j - 1];
+        g[0] = gf->log2exp[gf_mod(gf, (uint16_t)(gf->exp2log[g[0]] + root))];
+    }
+    for (uint16_t i = 0; i <= num_roots; i++)
+        g[i] = gf->exp2log[g[i]];
+    return rs;
+}
+
+/* ------------------------------------------------------------------------ */
+/* erasure list                                                             */
+/* ------------------------------------------------------------------------ */
+
+EXPORT void poporon_erasure_destroy(poporon_erasure_t *e)
+{
+    if (!e)
+        return;
+    free(e->erasure_positions);
+    free(e->corrections);
+    free(e);
+}
+
+EXPORT poporon_erasure_t *poporon_erasure_create(uint16_t num_roots, uint32_t initial_capacity)
+{
+    const uint32_t cap = initial_capacity > 0 ? initial_capacity : (uint32_t)num_roots;
+    poporon_erasure_t *e = (poporon_erasure_t *)calloc(1, sizeof(poporon_erasure_t));
+    if (!e)
+        return nullptr;
+    /* zero-filled (the reference leaves slots uninitialised; see quirk Q3) */
+    e->erasure_positions = (uint32_t *)calloc(cap ? cap : 1, sizeof(uint32_t));
+    e->corrections = (uint16_t *)calloc(cap ? cap : 1, sizeof(uint16_t));
+    if (!e->erasure_positions || !e->corrections) {
+        poporon_erasure_destroy(e);
+        return nullptr;
+    }
+    e->capacity = cap;
+    e->erasure_count = 0;
+    return e;
+}
+
+EXPORT poporon_erasure_t *poporon_erasure_create_from_positions(uint16_t num_roots, const uint32_t *positions,
+                                                                uint32_t count)
+{
+    if (!positions || count == 0)
+        return nullptr;
+    poporon_erasure_t *e = poporon_erasure_create(num_roots, count > num_roots ? count : num_roots);
+    if (!e)
+        return nullptr;
+    memcpy(e->erasure_positions, positions, (size_t)count * sizeof(uint32_t));
+    e->erasure_count = count;
+    return e;
+}
+
+EXPORT bool poporon_erasure_add_position(poporon_erasure_t *e, uint32_t position)
+{
+    if (!e)
+        return false;
+    if (e->erasure_count >= e->capacity) {
+        uint32_t cap = e->capacity * 2;
+        if (cap < e->capacity + 32)
+            cap = e->capacity + 32;
+        uint32_t *np = (uint32_t *)realloc(e->erasure_positions, (size_t)cap * sizeof(uint32_t));
+        if (!np)
+            return false;
+        e->erasure_positions = np;
+        uint16_t *nc = (uint16_t *)realloc(e->corrections, (size_t)cap * sizeof(uint16_t));
+        if (!nc)
+            return false;
+        e->corrections = nc;
+        memset(e->erasure_positions + e->capacity, 0, (size_t)(cap - e->capacity) * sizeof(uint32_t));
+        e->capacity = cap;
+    }
+    e->erasure_positions[e->erasure_count++] = position;
+    return true;
+}
+
+EXPORT void poporon_erasure_reset(poporon_erasure_t *e)
+{
+    if (e)
+        e->erasure_count = 0;
+}
+
+/* ------------------------------------------------------------------------ */
+/* configs                                                                  */
+/* ------------------------------------------------------------------------ */
+
+EXPORT poporon_config_t *poporon_rs_config_create(uint8_t symbol_size, uint16_t generator_polynomial,
+                                                  uint16_t first_consecutive_root, uint16_t primitive_element,
+                                                  uint8_t num_roots, poporon_erasure_t *erasure, uint16_t *syndrome)
+{
+    poporon_config_t *c = (poporon_config_t *)calloc(1, sizeof(poporon_config_t));
+    if (!c)
+        return nullptr;
+    c->fec_type = PPLN_FEC_RS;
+    c->symbol_size = symbol_size;
+    c->generator_polynomial = generator_polynomial;
+    c->first_consecutive_root = first_consecutive_root;
+    c->primitive_element = primitive_element;
+    c->num_roots = num_roots;
+    c->erasure = erasure;
+    c->syndrome = syndrome;
+    return c;
+}
+
+EXPORT poporon_config_t *poporon_config_rs_default(void)
+{
+    return poporon_rs_config_create(8, 0x11D, 1, 1, 32, nullptr, nullptr);
+}
+
+/* LDPC and BCH are outside this build's scope:
+ * exported so that callers link, but they construct nothing. */
+EXPORT poporon_config_t *poporon_ldpc_config_create(size_t, poporon_ldpc_rate_t, poporon_ldpc_matrix_type_t, uint32_t,
+                                                    bool, bool, bool, uint32_t, uint32_t, uint32_t, const int8_t *,
+                                                    size_t, uint64_t)
+{
+    fail("LDPC is not provided by libpoporon_amd");
+    return nullptr;
+}
+EXPORT poporon_config_t *poporon_bch_config_create(uint8_t, uint16_t, uint8_t)
+{
+    fail("BCH is not provided by libpoporon_amd");
+    return nullptr;
+}
+EXPORT poporon_config_t *poporon_config_ldpc_default(size_t, poporon_ldpc_rate_t)
+{
+    fail("LDPC is not provided by libpoporon_amd");
+    return nullptr;
+}
+EXPORT poporon_config_t *poporon_config_ldpc_burst_resistant(size_t, poporon_ldpc_rate_t)
+{
+    fail("LDPC is not provided by libpoporon_amd");
+    return nullptr;
+}
+EXPORT poporon_config_t *poporon_config_bch_default(void)
+{
+    fail("BCH is not provided by libpoporon_amd");
+    return nullptr;
+}
+
+EXPORT void poporon_config_destroy(poporon_config_t *config) { free(config); }
+
+/* ------------------------------------------------------------------------ */
+/* handle                                                                   */
+/* ------------------------------------------------------------------------ */
+
+/* Kernel tables for the handle (see rs_device.h for their definitions). */
+static void build_tables(poporon_t *h)
+{
+    const poporon_rs_t *rs = h->rs;
+    const poporon_gf_t *gf = rs->gf;
+    const uint16_t *g = rs->generator_polynomial;
+    RsDevTables &t = h->host_tab;
+    memset(&t, 0, sizeof(t));
+    uint8_t row[32];
+    for (uint32_t fb = 0; fb < 256; fb++) {
+        for (uint32_t m = 0; m < 32; m++)
+            row[m] = fb == 0 ? 0
+                             : (uint8_t)gf->log2exp[gf_mod(gf, (uint16_t)(gf->exp2log[fb] + g[RS_NR - 1 - m]))];
+        memcpy(&t.lfsr[fb * 2], row, 16);
+        memcpy(&t.lfsr[fb * 2 + 1], row + 16, 16);
+    }
+    for (uint32_t x = 0; x < 512; x++)
+        t.exp2[x] = (uint8_t)gf->log2exp[x % 255];
+    for (uint32_t v = 0; v < 256; v++)
+        t.log[v] = (uint8_t)gf->exp2log[v];
+
+    RsCorrParams &p = h->corr;
+    memset(&p, 0, sizeof(p));
+    p.fcr = rs->first_consecutive_root;
+    p.prim = rs->primitive_element;
+    p.iprim = h->primitive_inverse;
+    /* the LFSR computes c(x) x^32 mod g, so S_i = r(beta_i) beta_i^-32 =
+     * sum_m r_m beta_i^-(m+1), beta_i = alpha^(prim (fcr + i)) */
+    for (uint32_t m = 0; m < RS_NR; m++) {
+        const long long a = (long long)(m + 1) * p.prim;
+        p.tr_inc[m] = (uint8_t)((255 - (a % 255)) % 255);
+        p.tr_start[m] = (uint8_t)((255 - ((a * p.fcr) % 255)) % 255);
+    }
+}
+
+static bool params_supported(const poporon_t *h)
+{
+    const poporon_rs_t *rs = h->rs;
+    if (rs->gf->symbol_size != 8 || rs->num_roots != RS_NR || rs->primitive_element == 0)
+        return false;
+    if (((uint32_t)rs->first_consecutive_root + RS_NR - 1) * rs->primitive_element + 254u >= 65536u)
+        return false;
+    /* distinct roots: then "remainder == 0" <=> "all syndromes are zero" */
+    const uint32_t p = rs->primitive_element;
+    if (p % 3 == 0 || p % 5 == 0 || p % 17 == 0)
+        return false;
+    for (uint32_t i = 0; i < RS_NR; i++) /* the LFSR remainder needs a generator without zero coefficients */
+        if (rs->generator_polynomial[i] == rs->gf->field_size)
+            return false;
+    return true;
+}
+
+EXPORT poporon_t *poporon_create(const poporon_config_t *config)
+{
+    if (!config)
+        return nullptr;
+    if (config->fec_type != PPLN_FEC_RS) {
+        fail("only PPLN_FEC_RS is provided by libpoporon_amd");
+        return nullptr;
+    }
+    poporon_rs_t *rs = poporon_rs_create(config->symbol_size, config->generator_polynomial,
+                                         config->first_consecutive_root, config->primitive_element, config->num_roots);
+    if (!rs)
+        return nullptr;
+    if (config->primitive_element == 0) {
+        poporon_rs_destroy(rs);
+        return nullptr;
+    }
+    /* smallest 1 + j*field_size (uint16 arithmetic) divisible by prim, over prim */
+    uint32_t tries = 0;
+    uint16_t pi;
+    for (pi = 1; (pi % config->primitive_element) != 0; pi = (uint16_t)(pi + rs->gf->field_size)) {
+        if (++tries > (uint32_t)rs->gf->field_size * 2) {
+            poporon_rs_destroy(rs);
+            return nullptr;
+        }
+    }
+    poporon_t *h = new (std::nothrow) _poporon_t();
+    if (!h) {
+        poporon_rs_destroy(rs);
+        return nullptr;
+    }
+    h->fec_type = PPLN_FEC_RS;
+    h->rs = rs;
+    h->primitive_inverse = (uint16_t)(pi / config->primitive_element);
+    h->erasure = config->erasure;
+    h->ext_syndrome = config->syndrome;
+    h->last_corrected = 0;
+    h->supported = params_supported(h);
+    if (h->supported)
+        build_tables(h);
+    return h;
+}
+
+static void gpu_release(GpuCtx &g)
+{
+    if (!g.ready)
+        return;
+    int prev = -1;
+    (void)hipGetDevice(&prev);
+    (void)hipSetDevice(g.device);
+    if (g.stream)
+        (void)hipStreamSynchronize(g.stream);
+    for (auto &t : g.pending) {
+        (void)hipEventDestroy(t.a);
+        (void)hipEventDestroy(t.b);
+    }
+    for (auto e : g.event_pool)
+        (void)hipEventDestroy(e);
+    (void)hipFree(g.tab);
+    (void)hipFree(g.rem);
+    (void)hipFree(g.stage);
+    if (g.stream)
+        (void)hipStreamDestroy(g.stream);
+    if (prev >= 0)
+        (void)hipSetDevice(prev);
+    g = GpuCtx();
+}
+
+EXPORT void poporon_destroy(poporon_t *h)
+{
+    if (!h)
+        return;
+    gpu_release(h->gpu);
+    poporon_rs_destroy(h->rs);
+    delete h;
+}
+
+EXPORT poporon_fec_type_t poporon_get_fec_type(const poporon_t *h) { return h ? h->fec_type : PPLN_FEC_UNKNOWN; }
+EXPORT uint32_t poporon_get_iterations_used(const poporon_t *) { return 0; }
+EXPORT size_t poporon_get_parity_size(const poporon_t *h) { return h ? h->rs->num_roots : 0; }
+EXPORT size_t poporon_get_info_size(const poporon_t *h)
+{
+    return h ? (size_t)(h->rs->gf->field_size - h->rs->num_roots) : 0;
+}
+EXPORT uint32_t poporon_version_id(void) { return (uint32_t)POPORON_VERSION_ID; }
+EXPORT poporon_buildtime_t poporon_buildtime(void) { return (poporon_buildtime_t)POPORON_BUILDTIME; }
+
+/* ------------------------------------------------------------------------ */
+/* GPU context                                                              */
+/* ------------------------------------------------------------------------ */
+
+EXPORT int poporon_amd_device_count(void)
+{
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess)
+        return 0;
+    return n;
+}
+
+EXPORT bool poporon_amd_supported(const poporon_t *h) { return h && h->supported; }
+
+/* Scoped switch to the handle's device; restores the caller's device. */
+struct DeviceGuard {
+    int prev = -1;
+    bool ok = false;
+    explicit DeviceGuard(int dev)
+    {
+        if (hipGetDevice(&prev) != hipSuccess)
+            prev = -1;
+        ok = hipSetDevice(dev) == hipSuccess;
+    }
+    ~DeviceGuard()
+    {
+        if (prev >= 0)
+            (void)hipSetDevice(prev);
+    }
+};
+
+EXPORT bool poporon_amd_set_device(poporon_t *h, int device)
+{
+    if (!h)
+        return fail("NULL handle");
+    if (h->gpu.ready && h->gpu.device != device)
+        return fail("handle already bound to device %d", h->gpu.device);
+    int n = poporon_amd_device_count();
+    if (device < 0 || device >= n)
+        return fail("device %d out of range (%d HIP devices)", device, n);
+    h->gpu.device = device;
+    return true;
+}
+
+static bool gpu_init(poporon_t *h)
+{
+    GpuCtx &g = h->gpu;
+    if (g.ready)
+        return true;
+    if (!h->supported)
+        return fail("RS parameters not served by the GPU kernels (need symbol_size 8, num_roots 32, a generator "
+                    "without zero coefficients and (fcr+31)*prim+254 < 65536)");
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    if (e != hipSuccess || n == 0)
+        return fail("no HIP device available (%s); libpoporon_amd has no CPU fallback",
+                    e != hipSuccess ? hipGetErrorString(e) : "0 devices");
+    if (g.device < 0) {
+        int cur = 0;
+        HIP_OK(hipGetDevice(&cur));
+        g.device = cur;
+    }
+    DeviceGuard dg(g.device);
+    if (!dg.ok)
+        return fail("hipSetDevice(%d) failed", g.device);
+    hipDeviceProp_t prop;
+    HIP_OK(hipGetDeviceProperties(&prop, g.device));
+    g.num_cu = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
+    HIP_OK(hipStreamCreateWithFlags(&g.stream, hipStreamNonBlocking));
+    HIP_OK(hipMalloc((void **)&g.tab, sizeof(RsDevTables)));
+    HIP_OK(hipMemcpy(g.tab, &h->host_tab, sizeof(RsDevTables), hipMemcpyHostToDevice));
+    g.ready = true;
+    return true;
+}
+
+static bool ensure_rem(poporon_t *h, size_t count)
+{
+    GpuCtx &g = h->gpu;
+    if (g.rem_cap >= count)
+        return true;
+    size_t cap = std::max(count, (size_t)1024);
+    if (g.rem) {
+        HIP_OK(hipStreamSynchronize(g.stream));
+        HIP_OK(hipFree(g.rem));
+        g.rem = nullptr;
+        g.rem_cap = 0;
+    }
+    HIP_OK(hipMalloc((void **)&g.rem, cap * RS_NR));
+    g.rem_cap = cap;
+    return true;
+}
+
+static bool ensure_stage(poporon_t *h, size_t bytes)
+{
+    GpuCtx &g = h->gpu;
+    if (g.stage_cap >= bytes)
+        return true;
+    size_t cap = std::max(bytes, (size_t)4096);
+    if (g.stage) {
+        HIP_OK(hipStreamSynchronize(g.stream));
+        HIP_OK(hipFree(g.stage));
+        g.stage = nullptr;
+        g.stage_cap = 0;
+    }
+    HIP_OK(hipMalloc((void **)&g.stage, cap));
+    g.stage_cap = cap;
+    return true;
+}
+
+EXPORT bool poporon_amd_reserve(poporon_t *h, size_t max_count)
+{
+    if (!h)
+        return fail("NULL handle");
+    if (!gpu_init(h))
+        return false;
+    DeviceGuard dg(h->gpu.device);
+    return ensure_rem(h, max_count);
+}
+
+static bool check_decode_size(const poporon_t *h, size_t size)
+{
+    /* src/decode.c:418-429: pad = nn - nroots - size must lie in [0, nn - nroots) */
+    const size_t kmax = (size_t)h->rs->gf->field_size - h->rs->num_roots;
+    return size >= 1 && size <= kmax;
+}
+
+/* ------------------------------------------------------------------------ */
+/* in-library kernel timing (HIP events on the launch stream)               */
+/* ------------------------------------------------------------------------ */
+
+static hipEvent_t take_event(GpuCtx &g)
+{
+    hipEvent_t e = nullptr;
+    if (!g.event_pool.empty()) {
+        e = g.event_pool.back();
+        g.event_pool.pop_back();
+    } else if (hipEventCreate(&e) != hipSuccess) {
+        e = nullptr;
+    }
+    return e;
+}
+
+/* Bracket one launch with events when timing is on. */
+struct KernelTimer {
+    GpuCtx &g;
+    int kernel;
+    hipStream_t s;
+    hipEvent_t a = nullptr, b = nullptr;
+    KernelTimer(GpuCtx &g_, int k, hipStream_t s_) : g(g_), kernel(k), s(s_)
+    {
+        if (g.timing && (a = take_event(g)) != nullptr)
+            (void)hipEventRecord(a, s);
+    }
+    void done()
+    {
+        if (!a)
+            return;
+        if ((b = take_event(g)) != nullptr && hipEventRecord(b, s) == hipSuccess)
+            g.pending.push_back({kernel, a, b});
+        else
+            g.event_pool.push_back(a);
+        a = nullptr;
+    }
+};
+
+static bool drain_timing(GpuCtx &g)
+{
+    for (auto &t : g.pending) {
+        float ms = 0.f;
+        HIP_OK(hipEventSynchronize(t.b));
+        HIP_OK(hipEventElapsedTime(&ms, t.a, t.b));
+        g.total_ms[t.kernel] += ms;
+        g.launches[t.kernel] += 1;
+        g.event_pool.push_back(t.a);
+        g.event_pool.push_back(t.b);
+    }
+    g.pending.clear();
+    return true;
+}
+
+EXPORT bool poporon_amd_timing(poporon_t *h, int enable)
+{
+    if (!h)
+        return fail("NULL handle");
+    if (!gpu_init(h))
+        return false;
+    DeviceGuard dg(h->gpu.device);
+    GpuCtx &g = h->gpu;
+    if (!drain_timing(g))
+        return false;
+    for (int k = 0; k < NKERN; k++) {
+        g.total_ms[k] = 0;
+        g.launches[k] = 0;
+    }
+    g.timing = enable != 0;
+    return true;
+}
+
+EXPORT bool poporon_amd_timing_read(poporon_t *h, int kernel, double *total_ms, uint64_t *launches)
+{
+    if (!h || kernel < 0 || kernel >= NKERN)
+        return fail("bad handle or kernel id");
+    if (!h->gpu.ready)
+        return fail("no GPU work recorded");
+    DeviceGuard dg(h->gpu.device);
+    if (!drain_timing(h->gpu))
+        return false;
+    if (total_ms)
+        *total_ms = h->gpu.total_ms[kernel];
+    if (launches)
+        *launches = h->gpu.launches[kernel];
+    return true;
+}
+
+/* ------------------------------------------------------------------------ */
+/* device batches                                                           */
+/* ------------------------------------------------------------------------ */
+
+static bool launch_encode(poporon_t *h, const uint8_t *d_data, size_t ds, uint8_t *d_par, size_t ps, size_t size,
+                          size_t count, hipStream_t s)
+{
+    KernelTimer t(h->gpu, POPORON_AMD_KERNEL_ENCODE, s);
+    HIP_OK(rsk_encode(h->gpu.tab, d_data, ds, d_par, ps, (uint32_t)size, count, h->gpu.num_cu, s));
+    t.done();
+    return true;
+}
+
+static bool launch_decode(poporon_t *h, uint8_t *d_data, size_t ds, uint8_t *d_par, size_t ps, size_t size,
+                          size_t count, const uint8_t *ext_syn, const uint8_t *pos8, const uint32_t *pos32,
+                          size_t pos_stride, const uint8_t *cnt, uint8_t *ok, uint8_t *corrected, hipStream_t s)
+{
+    RsCorrParams prm = h->corr;
+    prm.size = (uint32_t)size;
+    prm.pad = (int32_t)(h->rs->gf->field_size - h->rs->num_roots - size);
+    if (!ext_syn) {
+        if (!ensure_rem(h, count))
+            return false;
+        KernelTimer t(h->gpu, POPORON_AMD_KERNEL_REMAINDER, s);
+        HIP_OK(rsk_remainder(h->gpu.tab, d_data, ds, d_par, ps, (uint32_t)size, count, h->gpu.rem, h->gpu.num_cu, s));
+        t.done();
+    }
+    KernelTimer t(h->gpu, POPORON_AMD_KERNEL_CORRECT, s);
+    HIP_OK(rsk_correct(h->gpu.tab, &prm, d_data, ds, d_par, ps, count, ext_syn ? nullptr : h->gpu.rem, ext_syn, pos8,
+                       pos32, pos_stride, cnt, ok, corrected, s));
+    t.done();
+    return true;
+}
+
+EXPORT bool poporon_check_batch_device(poporon_t *h, const uint8_t *d_data, size_t data_stride,
+                                       const uint8_t *d_parity, size_t parity_stride, size_t size, size_t count,
+                                       uint8_t *d_dirty, void *stream)
+{
+    if (!h || (count && (!d_data || !d_parity || !d_dirty)))
+        return fail("NULL argument");
+    if (!check_decode_size(h, size))
+        return fail("size %zu outside [1, %u]", size, (unsigned)(h->rs->gf->field_size - h->rs->num_roots));
+    if (!gpu_init(h))
+        return false;
+    DeviceGuard dg(h->gpu.device);
+    hipStream_t s = (hipStream_t)stream;
+    KernelTimer t(h->gpu, POPORON_AMD_KERNEL_CHECK, s);
+    HIP_OK(rsk_check(h->gpu.tab, d_data, data_stride, d_parity, parity_stride, (uint32_t)size, count, d_dirty,
+                     h->gpu.num_cu, s));
+    t.done();
+    return true;
+}
+
+EXPORT bool poporon_encode_batch_device(poporon_t *h, const uint8_t *d_data, size_t data_stride, uint8_t *d_parity,
+                                        size_t parity_stride, size_t size, size_t count, void *stream)
+{
+    if (!h || (count && (!d_data || !d_parity)))
+        return fail("NULL argument");
+    if (size > 65535)
+        return fail("size %zu > 65535 (the reference's uint16 byte counter never terminates)", size);
+    if (!gpu_init(h))
+        return false;
+    DeviceGuard dg(h->gpu.device);
+    return launch_encode(h, d_data, data_stride, d_parity, parity_stride, size, count, (hipStream_t)stream);
+}
+
+EXPORT bool poporon_decode_batch_device(poporon_t *h, uint8_t *d_data, size_t data_stride, uint8_t *d_parity,
+                                        size_t parity_stride, size_t size, size_t count, const uint8_t *d_positions,
+                                        size_t positions_stride, const uint8_t *d_counts, uint8_t *d_ok,
+                                        uint8_t *d_corrected, void *stream)
+{
+    if (!h || (count && (!d_data || !d_parity || !d_ok)))
+        return fail("NULL argument");
+    if (d_positions && (!d_counts || positions_stride < RS_NR))
+        return fail("erasure batch needs counts and positions_stride >= %d", RS_NR);
+    if (!check_decode_size(h, size))
+        return fail("decode size %zu outside [1, %u]", size, (unsigned)(h->rs->gf->field_size - h->rs->num_roots));
+    if (!gpu_init(h))
+        return false;
+    DeviceGuard dg(h->gpu.device);
+    return launch_decode(h, d_data, data_stride, d_parity, parity_stride, size, count, nullptr, d_positions, nullptr,
+                         positions_stride, d_counts, d_ok, d_corrected, (hipStream_t)stream);
+}
+
+/* ------------------------------------------------------------------------ */
+/* host batches: staged through device memory in chunks                     */
+/* ------------------------------------------------------------------------ */
+
+static const size_t kHostChunk = 1u << 20; /* codewords per staged chunk */
+
+static void gather(uint8_t *dst, const uint8_t *src, size_t stride, size_t width, size_t count)
+{
+    if (stride == width) {
+        memcpy(dst, src, width * count);
+        return;
+    }
+    for (size_t c = 0; c < count; c++)
+        memcpy(dst + c * width, src + c * stride, width);
+}
+
+static void scatter(uint8_t *dst, size_t stride, const uint8_t *src, size_t width, size_t count)
+{
+    if (stride == width) {
+        memcpy(dst, src, width * count);
+        return;
+    }
+    for (size_t c = 0; c < count; c++)
+        memcpy(dst + c * stride, src + c * width, width);
+}
+
+EXPORT bool poporon_encode_batch(poporon_t *h, const uint8_t *data, size_t data_stride, uint8_t *parity,
+                                 size_t parity_stride, size_t size, size_t count)
+{
+    if (!h || (count && (!data || !parity)))
+        return fail("NULL argument");
+    if (size > 65535)
+        return fail("size %zu > 65535", size);
+    if (!gpu_init(h))
+        return false;
+    DeviceGuard dg(h->gpu.device);
+    GpuCtx &g = h->gpu;
+    const size_t nr = h->rs->num_roots;
+    const size_t chunk = std::min(count, kHostChunk);
+    if (!ensure_stage(h, chunk * (size + nr) + 16))
+        return false;
+    std::vector<uint8_t> tmp(chunk * (size + nr));
+    for (size_t c0 = 0; c0 < count; c0 += chunk) {
+        const size_t n = std::min(chunk, count - c0);
+        gather(tmp.data(), data + c0 * data_stride, data_stride, size, n);
+        uint8_t *dd = g.stage, *dp = g.stage + n * size;
+        HIP_OK(hipMemcpyAsync(dd, tmp.data(), n * size, hipMemcpyHostToDevice, g.stream));
+        if (!launch_encode(h, dd, size, dp, nr, size, n, g.stream))
+            return false;
+        HIP_OK(hipMemcpyAsync(tmp.data(), dp, n * nr, hipMemcpyDeviceToHost, g.stream));
+        HIP_OK(hipStreamSynchronize(g.stream));
+        scatter(parity + c0 * parity_stride, parity_stride, tmp.data(), nr, n);
+    }
+    return true;
+}
+
+EXPORT bool poporon_decode_batch(poporon_t *h, uint8_t *data, size_t data_stride, uint8_t *parity,
+                                 size_t parity_stride, size_t size, size_t count, const uint8_t *positions,
+                                 size_t positions_stride, const uint8_t *counts, uint8_t *ok, uint8_t *corrected)
+{
+    if (!h || (count && (!data || !parity || !ok)))
+        return fail("NULL argument");
+    if (positions && (!counts || positions_stride < RS_NR))
+        return fail("erasure batch needs counts and positions_stride >= %d", RS_NR);
+    if (!check_decode_size(h, size))
+        return fail("decode size %zu outside [1, %u]", size, (unsigned)(h->rs->gf->field_size - h->rs->num_roots));
+    if (!gpu_init(h))
+        return false;
+    DeviceGuard dg(h->gpu.device);
+    GpuCtx &g = h->gpu;
+    const size_t nr = h->rs->num_roots;
+    const size_t chunk = std::min(count, kHostChunk);
+    const size_t per = size + nr + 2 + (positions ? RS_NR + 1 : 0);
+    if (!ensure_stage(h, chunk * per + 64))
+        return false;
+    std::vector<uint8_t> tmp(chunk * (size + nr + RS_NR + 1));
+    for (size_t c0 = 0; c0 < count; c0 += chunk) {
+        const size_t n = std::min(chunk, count - c0);
+        uint8_t *dd = g.stage, *dp = dd + n * size, *dok = dp + n * nr, *dcor = dok + n, *dpos = dcor + n,
+                *dcnt = dpos + (positions ? n * RS_NR : 0);
+        gather(tmp.data(), data + c0 * data_stride, data_stride, size, n);
+        gather(tmp.data() + n * size, parity + c0 * parity_stride, parity_stride, nr, n);
+        HIP_OK(hipMemcpyAsync(dd, tmp.data(), n * (size + nr), hipMemcpyHostToDevice, g.stream));
+        if (positions) {
+            std::vector<uint8_t> pt(n * RS_NR);
+            gather(pt.data(), positions + c0 * positions_stride, positions_stride, RS_NR, n);
+            HIP_OK(hipMemcpyAsync(dpos, pt.data(), n * RS_NR, hipMemcpyHostToDevice, g.stream));
+            HIP_OK(hipMemcpyAsync(dcnt, counts + c0, n, hipMemcpyHostToDevice, g.stream));
+            HIP_OK(hipStreamSynchronize(g.stream));
+        }
+        if (!launch_decode(h, dd, size, dp, nr, size, n, nullptr, positions ? dpos : nullptr, nullptr, RS_NR,
+                           positions ? dcnt : nullptr, dok, dcor, g.stream))
+            return false;
+        HIP_OK(hipMemcpyAsync(tmp.data(), dd, n * (size + nr), hipMemcpyDeviceToHost, g.stream));
+        HIP_OK(hipMemcpyAsync(ok + c0, dok, n, hipMemcpyDeviceToHost, g.stream));
+        if (corrected)
+            HIP_OK(hipMemcpyAsync(corrected + c0, dcor, n, hipMemcpyDeviceToHost, g.stream));
+        HIP_OK(hipStreamSynchronize(g.stream));
+        scatter(data + c0 * data_stride, data_stride, tmp.data(), size, n);
+        scatter(parity + c0 * parity_stride, parity_stride, tmp.data() + n * size, nr, n);
+    }
+    return true;
+}
+
+/* ------------------------------------------------------------------------ */
+/* single-codeword API (the reference's entry points): a batch of one       */
+/* ------------------------------------------------------------------------ */
+
+EXPORT bool poporon_encode(poporon_t *h, uint8_t *data, size_t size, uint8_t *parity)
+{
+    if (!h || !data || !parity)
+        return false;
+    if (h->fec_type != PPLN_FEC_RS)
+        return false;
+    if (size > 65535) /* the reference's uint16 counter loops forever here (quirk Q7) */
+        return fail("size %zu > 65535", size);
+    if (!gpu_init(h))
+        return false;
+    DeviceGuard dg(h->gpu.device);
+    GpuCtx &g = h->gpu;
+    const size_t nr = h->rs->num_roots;
+    if (!ensure_stage(h, size + nr + 16))
+        return false;
+    uint8_t *dd = g.stage, *dp = g.stage + ((size + 15) & ~(size_t)15);
+    if (size)
+        HIP_OK(hipMemcpyAsync(dd, data, size, hipMemcpyHostToDevice, g.stream));
+    if (!launch_encode(h, dd, size, dp, nr, size, 1, g.stream))
+        return false;
+    HIP_OK(hipMemcpyAsync(parity, dp, nr, hipMemcpyDeviceToHost, g.stream));
+    HIP_OK(hipStreamSynchronize(g.stream));
+    return true;
+}
+
+EXPORT bool poporon_decode(poporon_t *h, uint8_t *data, size_t size, uint8_t *parity, size_t *corrected_num)
+{
+    if (!h || !data || !parity || !size)
+        return false;
+    if (h->fec_type != PPLN_FEC_RS)
+        return false;
+    size_t fixed = 0;
+    bool success = false;
+    if (!check_decode_size(h, size)) {
+        h->last_corrected = 0;
+        if (corrected_num)
+            *corrected_num = 0;
+        return false;
+    }
+    if (!gpu_init(h)) {
+        h->last_corrected = 0;
+        if (corrected_num)
+            *corrected_num = 0;
+        return false;
+    }
+    {
+        DeviceGuard dg(h->gpu.device);
+        GpuCtx &g = h->gpu;
+        const size_t nr = h->rs->num_roots;
+        /* stage layout: [data | parity | ok | cor | pad | syn(32) or slots(32 x u32) | count] */
+        const size_t off_p = size, off_ok = size + nr, off_cor = off_ok + 1;
+        const size_t off_x = (off_cor + 1 + 15) & ~(size_t)15;
+        if (!ensure_stage(h, off_x + RS_NR * 4 + 16))
+            return false;
+        uint8_t hostbuf[RS_NR * 4 + 16];
+        const uint8_t *ext = nullptr;
+        const uint32_t *pos32 = nullptr;
+        const uint8_t *cnt = nullptr;
+        bool refuse = false;
+        HIP_OK(hipMemcpyAsync(g.stage, data, size, hipMemcpyHostToDevice, g.stream));
+        HIP_OK(hipMemcpyAsync(g.stage + off_p, parity, nr, hipMemcpyHostToDevice, g.stream));
+        if (h->ext_syndrome) {
+            for (size_t i = 0; i < nr; i++) {
+                if (h->ext_syndrome[i] > 255)
+                    refuse = true; /* out-of-table index in the reference */
+                hostbuf[i] = (uint8_t)h->ext_syndrome[i];
+            }
+            HIP_OK(hipMemcpyAsync(g.stage + off_x, hostbuf, nr, hipMemcpyHostToDevice, g.stream));
+            ext = g.stage + off_x;
+        } else if (h->erasure) {
+            const poporon_erasure_t *e = h->erasure;
+            uint32_t slots[RS_NR];
+            memset(slots, 0, sizeof(slots));
+            memcpy(slots, e->erasure_positions, std::min<size_t>(e->capacity, RS_NR) * sizeof(uint32_t));
+            if (e->erasure_count > RS_NR)
+                refuse = true; /* quirk Q5: overflows the locator in the reference */
+            memcpy(hostbuf, slots, sizeof(slots));
+            hostbuf[RS_NR * 4] = (uint8_t)std::min<uint32_t>(e->erasure_count, 255u);
+            HIP_OK(hipMemcpyAsync(g.stage + off_x, hostbuf, RS_NR * 4 + 1, hipMemcpyHostToDevice, g.stream));
+            pos32 = (const uint32_t *)(g.stage + off_x);
+            cnt = g.stage + off_x + RS_NR * 4;
+        }
+        if (refuse) {
+            HIP_OK(hipStreamSynchronize(g.stream));
+            fail("erasure count > num_roots or external syndrome > 255: undefined in the reference, refused");
+        } else {
+            if (!launch_decode(h, g.stage, size, g.stage + off_p, nr, size, 1, ext, nullptr, pos32, RS_NR, cnt,
+                               g.stage + off_ok, g.stage + off_cor, g.stream))
+                return false;
+            uint8_t res[2];
+            HIP_OK(hipMemcpyAsync(data, g.stage, size, hipMemcpyDeviceToHost, g.stream));
+            HIP_OK(hipMemcpyAsync(parity, g.stage + off_p, nr, hipMemcpyDeviceToHost, g.stream));
+            HIP_OK(hipMemcpyAsync(res, g.stage + off_ok, 2, hipMemcpyDeviceToHost, g.stream));
+            HIP_OK(hipStreamSynchronize(g.stream));
+            success = res[0] != 0;
+            fixed = res[1];
+        }
+    }
+    h->last_corrected = fixed;
+    if (corrected_num)
+        *corrected_num = fixed;
+    return success;
+}

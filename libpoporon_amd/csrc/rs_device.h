@@ -1,0 +1,79 @@
+/*
+ * rs_device.h -- parameter blocks shared by the host library and the HIP
+ * kernels of libpoporon_amd (RS(n, n-32) over GF(2^8), gfx950).
+ */
+#ifndef POPORON_AMD_RS_DEVICE_H
+#define POPORON_AMD_RS_DEVICE_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#include <hip/hip_runtime.h>
+
+#define RS_NR 32      /* num_roots served by the kernels */
+#define RS_A0 255u    /* log of zero */
+#define RS_NN 255u    /* field size - 1 */
+
+/*
+ * Device-resident per-handle tables (one hipMalloc, built on the host by
+ * rs_tables.cpp from the handle's GF tables and generator polynomial).
+ *
+ *  lfsr[fb*2 + h]  : 16-byte half h of the 32-byte LFSR row for feedback byte
+ *                    fb: byte m = alpha^(log fb + g[31-m]) with the
+ *                    reference's gf_mod semantics (src/encode.c:126-140), so
+ *                    that  P' = (P >> 8 bits) ^ row[fb]  is one encode step.
+ *  exp2[x]         : alpha^(x mod 255) for x < 512 (exp2[255] = 1).
+ *  log[v]          : discrete log, log[0] = 255.
+ */
+struct RsDevTables {
+    uint4 lfsr[512];
+    uint8_t exp2[512];
+    uint8_t log[256];
+};
+
+/*
+ * Parameters of the correction kernel (by value).  tr_start/tr_inc turn the
+ * 32-byte remainder r (byte m = coefficient of x^(31-m)) into the syndromes
+ * S_i = r(beta_i), beta_i = alpha^(prim*(fcr+i)):
+ *   log(r_m * beta_i^(31-m)) = log r_m + tr_start[m] + i*tr_inc[m]  (mod 255).
+ */
+struct RsCorrParams {
+    uint32_t fcr, prim, iprim;
+    uint32_t size;   /* message bytes per codeword (1..223) */
+    int32_t pad;     /* 255 - 32 - size */
+    uint8_t tr_start[RS_NR];
+    uint8_t tr_inc[RS_NR];
+};
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Launchers (rs_kernels.hip).  All asynchronous on `stream`. */
+hipError_t rsk_encode(const RsDevTables *tab, const uint8_t *data, size_t dstride, uint8_t *parity, size_t pstride,
+                      uint32_t size, size_t count, int num_cu, hipStream_t stream);
+
+/* remainder of (data || parity) mod g, 32 bytes per codeword into rem */
+hipError_t rsk_remainder(const RsDevTables *tab, const uint8_t *data, size_t dstride, const uint8_t *parity,
+                         size_t pstride, uint32_t size, size_t count, uint8_t *rem, int num_cu, hipStream_t stream);
+
+/* flag[c] = remainder of codeword c is nonzero */
+hipError_t rsk_check(const RsDevTables *tab, const uint8_t *data, size_t dstride, const uint8_t *parity, size_t pstride,
+                     uint32_t size, size_t count, uint8_t *flag, int num_cu, hipStream_t stream);
+
+/*
+ * Correction.  Exactly one of rem / ext_syn is non-NULL (ext_syn: 32 log-form
+ * syndromes per codeword, the config's "syndrome" pointer path).  pos8 / pos32
+ * (at most one non-NULL) select erasure mode with per-codeword slot arrays of
+ * pos_stride entries and counts in cnt.
+ */
+hipError_t rsk_correct(const RsDevTables *tab, const RsCorrParams *prm, uint8_t *data, size_t dstride, uint8_t *parity,
+                       size_t pstride, size_t count, const uint8_t *rem, const uint8_t *ext_syn, const uint8_t *pos8,
+                       const uint32_t *pos32, size_t pos_stride, const uint8_t *cnt, uint8_t *ok, uint8_t *corrected,
+                       hipStream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif

@@ -1,0 +1,141 @@
+"""CPU checks of the C-ABI library (no GPU compute).
+
+* libpoporon_amd.so loads and exports every function include/*.h declares;
+* the host-side objects behave like the reference's: configs, handle getters,
+  version/buildtime (tests/test_basic.c:28-36), create(NULL)/destroy(NULL)
+  (tests/test_invalid.c:28-32), erasure lists (tests/test_erasure.c:30-104),
+  GF handle (tests/test_gf.c:31-79), RS create (tests/test_rs.c:36-83);
+* without a GPU the codec entry points fail loudly (no CPU fallback).
+"""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+import libpoporon_amd as P
+
+
+@pytest.fixture(scope="module")
+def lib():
+    return P.load_library()
+
+
+def test_exports_every_header_symbol(lib):
+    names = P.header_symbols()
+    assert len(names) >= 38
+    missing = [n for n in names if not hasattr(lib, n)]
+    assert not missing, missing
+    # the reference's public RS surface is all there
+    for n in ("poporon_rs_config_create", "poporon_config_rs_default", "poporon_create", "poporon_destroy",
+              "poporon_encode", "poporon_decode", "poporon_get_fec_type", "poporon_get_parity_size",
+              "poporon_get_info_size", "poporon_get_iterations_used", "poporon_version_id", "poporon_buildtime",
+              "poporon_erasure_create", "poporon_erasure_create_from_positions", "poporon_erasure_add_position",
+              "poporon_erasure_reset", "poporon_erasure_destroy", "poporon_gf_create", "poporon_gf_destroy",
+              "poporon_gf_mod"):
+        assert n in names
+
+
+def test_version_buildtime(lib, golden):
+    assert lib.poporon_version_id() == int(golden["version_id"][0]) == 20000000
+    assert lib.poporon_buildtime() > 0
+
+
+def test_invalid_handles(lib):
+    assert not lib.poporon_create(None)
+    lib.poporon_destroy(None)
+    assert lib.poporon_get_fec_type(None) == P.POPORON_FEC_UNKNOWN
+    assert lib.poporon_get_parity_size(None) == 0
+    assert lib.poporon_get_info_size(None) == 0
+    assert not lib.poporon_encode(None, None, 0, None)
+    assert not lib.poporon_decode(None, None, 0, None, None)
+
+
+def test_out_of_scope_codecs_return_null(lib):
+    assert not lib.poporon_config_bch_default()
+    assert not lib.poporon_config_ldpc_default(64, 1)
+    assert not lib.poporon_bch_config_create(4, 0x13, 3)
+
+
+def test_rs_handle_getters():
+    h = P.Poporon.default()
+    assert h.fec_type == P.POPORON_FEC_RS
+    assert h.parity_size == 32
+    assert h.info_size == 223
+    assert h.lib.poporon_get_iterations_used(h.h) == 0
+    assert h.supported
+    h16 = P.Poporon(8, 0x11D, 1, 1, 16)
+    assert h16.parity_size == 16 and h16.info_size == 239
+    assert not h16.supported  # the GPU kernels serve num_roots == 32
+    with pytest.raises(P.PoporonError):
+        P.Poporon(8, 0x11C, 1, 1, 32)  # non-primitive field polynomial -> NULL
+    with pytest.raises(P.PoporonError):
+        P.Poporon(8, 0x11D, 1, 0, 32)  # primitive_element 0 -> NULL
+
+
+def test_config_destroy_after_create_keeps_handle():
+    # tests/test_codec.c:30-38: the config may be destroyed right after create
+    h = P.Poporon.default()
+    assert h.parity_size == 32
+
+
+def test_erasure_api(lib):
+    e = P.Erasure(32, 8)
+    for i in range(18):
+        assert e.add(i)
+    assert not lib.poporon_erasure_add_position(None, 0)
+    e.reset()
+    for i in range(5):
+        assert e.add(i)
+    lib.poporon_erasure_reset(None)
+    e.close()
+    lib.poporon_erasure_destroy(None)
+    assert P.Erasure(32, 0).h
+    arr = np.array([1, 3, 5, 7, 9], np.uint32)
+    assert lib.poporon_erasure_create_from_positions(32, arr.ctypes.data_as(C.c_void_p), 5)
+    assert not lib.poporon_erasure_create_from_positions(32, None, 5)
+    assert not lib.poporon_erasure_create_from_positions(32, arr.ctypes.data_as(C.c_void_p), 0)
+
+
+def test_gf_api(lib, golden):
+    g = lib.poporon_gf_create(8, 0x11D)
+    assert g
+    for v, want in zip(golden["gf_mod_in"], golden["gf_mod_out"]):
+        assert lib.poporon_gf_mod(g, int(v)) == want
+    for v in range(255):
+        assert lib.poporon_gf_mod(g, v) == v
+    lib.poporon_gf_destroy(g)
+    assert lib.poporon_gf_create(4, 0x13)
+    assert not lib.poporon_gf_create(0, 0x11D)
+    assert not lib.poporon_gf_create(17, 0x11D)
+    lib.poporon_gf_destroy(None)
+
+
+def test_rs_create_api(lib):
+    for args in ((8, 0x11D, 1, 1, 16), (4, 0x13, 1, 2, 8), (8, 0x11D, 1, 1, 4), (8, 0x11D, 1, 1, 8),
+                 (8, 0x11D, 1, 1, 32), (8, 0x11D, 0, 1, 16), (8, 0x11D, 2, 1, 16), (8, 0x11D, 1, 2, 16)):
+        rs = lib.poporon_rs_create(*args)
+        assert rs
+        lib.poporon_rs_destroy(rs)
+    assert not lib.poporon_rs_create(0, 0x11D, 1, 1, 16)
+    lib.poporon_rs_destroy(None)
+
+
+def test_no_gpu_fails_loudly():
+    if P.device_count() > 0:
+        pytest.skip("GPU present")
+    h = P.Poporon.default()
+    with pytest.raises(P.PoporonError, match="no CPU fallback"):
+        h.encode(np.zeros(223, np.uint8))
+    ok, n, _, _ = h.decode(np.zeros(223, np.uint8), np.zeros(32, np.uint8))
+    assert not ok and n == 0
+    assert "no CPU fallback" in P.last_error()
+    with pytest.raises(P.PoporonError):
+        h.encode_batch(np.zeros((4, 223), np.uint8))
+
+
+def test_shard_range_partitions():
+    for count in (0, 1, 7, 1 << 20, (1 << 20) + 3):
+        for world in (1, 2, 3, 4, 8):
+            got = [P.shard_range(count, r, world) for r in range(world)]
+            assert got[0][0] == 0 and got[-1][1] == count
+            assert all(got[i][1] == got[i + 1][0] for i in range(world - 1))

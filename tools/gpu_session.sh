@@ -1,0 +1,33 @@
+#!/bin/bash
+# tools/gpu_session.sh STEP... -- run GPU steps on the gpurun box, each under
+# its own time limit, stopping at the first fault/abort/timeout (exit codes
+# other than 0 = ok and 1 = test/assert failure).  Logs go to gpurun_out/.
+#   steps: smoke | tests | bench | prof | pmc
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+run() { # name limit cmd...
+    local name=$1 lim=$2
+    shift 2
+    echo "== $name: $*" | tee -a gpurun_out/session.log
+    timeout -k 10 "$lim" "$@" > "gpurun_out/$name.log" 2>&1
+    local rc=$?
+    echo "== $name rc=$rc" | tee -a gpurun_out/session.log
+    tail -n 25 "gpurun_out/$name.log"
+    if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then
+        echo "== stopping: $name exited $rc" | tee -a gpurun_out/session.log
+        exit $rc
+    fi
+    return 0
+}
+for step in "$@"; do
+    case $step in
+    smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    tests) run tests 900 python -m pytest tests -m gpu -x -q ;;
+    tests_all) run tests_all 900 python -m pytest tests -m gpu -q ;;
+    bench) run bench 600 python bench.py ;;
+    prof) run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- \
+        python3 bench.py --no-cpu-baseline --steps 10 ;;
+    *) echo "unknown step $step"; exit 2 ;;
+    esac
+done
