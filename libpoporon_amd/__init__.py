@@ -99,6 +99,13 @@ def load_library(path: str = LIB_PATH):
         return _lib
     if not os.path.exists(path):
         raise ImportError(f"{path} not found: build it with `make -C libpoporon_amd` (hipcc, gfx950)")
+    # One HIP runtime per process: torch ships its own libamdhip64.so.7.  If
+    # this library bound /opt/rocm's copy first, torch's HIP init would fail,
+    # so let torch (when installed) load the runtime and share it.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     lib = C.CDLL(path)
     for name, (res, args) in _SIGS.items():
         fn = getattr(lib, name)
