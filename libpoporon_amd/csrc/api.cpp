@@ -405,12 +405,40 @@ static void build_tables(poporon_t *h)
     p.fcr = rs->first_consecutive_root;
     p.prim = rs->primitive_element;
     p.iprim = h->primitive_inverse;
+    p.vfast = ((uint64_t)(p.fcr + RS_NR - 1) * p.prim * 254u) < 32768u;
     /* the LFSR computes c(x) x^32 mod g, so S_i = r(beta_i) beta_i^-32 =
      * sum_m r_m beta_i^-(m+1), beta_i = alpha^(prim (fcr + i)) */
     for (uint32_t m = 0; m < RS_NR; m++) {
         const long long a = (long long)(m + 1) * p.prim;
         p.tr_inc[m] = (uint8_t)((255 - (a % 255)) % 255);
         p.tr_start[m] = (uint8_t)((255 - ((a * p.fcr) % 255)) % 255);
+    }
+
+    /* remainder -> syndrome nibble tables (rs_device.h) */
+    auto gmul = [&](uint32_t x, uint32_t logc) -> uint8_t {
+        return x == 0 ? 0 : (uint8_t)gf->log2exp[(gf->exp2log[x] + logc) % 255];
+    };
+    for (uint32_t m = 0; m < RS_NR; m++) {
+        for (uint32_t n = 0; n < 2; n++) {
+            for (uint32_t v = 0; v < 16; v++) {
+                uint8_t rowb[RS_NR];
+                for (uint32_t i = 0; i < RS_NR; i++) {
+                    const uint64_t e = (uint64_t)(m + 1) * p.prim * (p.fcr + i);
+                    rowb[i] = gmul(v << (4 * n), (uint32_t)((255 - (e % 255)) % 255));
+                }
+                memcpy(&t.synt[((m * 2 + n) * 2 + 0) * 16 + v], rowb, 16);
+                memcpy(&t.synt[((m * 2 + n) * 2 + 1) * 16 + v], rowb + 16, 16);
+            }
+        }
+    }
+    /* Chien chunk rows: term j at 16 consecutive points */
+    for (uint32_t j = 1; j <= 16; j++) {
+        for (uint32_t e = 0; e < 255; e++) {
+            uint8_t rowb[16];
+            for (uint32_t b = 0; b < 16; b++)
+                rowb[b] = (uint8_t)gf->log2exp[(e + j * b) % 255];
+            memcpy(&t.chien[(j - 1) * 255 + e], rowb, 16);
+        }
     }
 }
 
@@ -755,12 +783,12 @@ static bool launch_decode(poporon_t *h, uint8_t *d_data, size_t ds, uint8_t *d_p
         if (!ensure_rem(h, count))
             return false;
         KernelTimer t(h->gpu, POPORON_AMD_KERNEL_REMAINDER, s);
-        HIP_OK(rsk_remainder(h->gpu.tab, d_data, ds, d_par, ps, (uint32_t)size, count, h->gpu.rem, h->gpu.num_cu, s));
+        HIP_OK(rsk_syndrome(h->gpu.tab, d_data, ds, d_par, ps, (uint32_t)size, count, h->gpu.rem, h->gpu.num_cu, s));
         t.done();
     }
     KernelTimer t(h->gpu, POPORON_AMD_KERNEL_CORRECT, s);
-    HIP_OK(rsk_correct(h->gpu.tab, &prm, d_data, ds, d_par, ps, count, ext_syn ? nullptr : h->gpu.rem, ext_syn, pos8,
-                       pos32, pos_stride, cnt, ok, corrected, s));
+    HIP_OK(rsk_correct(h->gpu.tab, &prm, d_data, ds, d_par, ps, count, ext_syn ? ext_syn : h->gpu.rem,
+                       ext_syn ? 1 : 0, pos8, pos32, pos_stride, cnt, ok, corrected, h->gpu.num_cu, s));
     t.done();
     return true;
 }

@@ -29,6 +29,17 @@ struct RsDevTables {
     uint4 lfsr[512];
     uint8_t exp2[512];
     uint8_t log[256];
+    /* synt: remainder -> syndromes, nibble tables.  For remainder byte m,
+     * nibble half n (0 = low, 1 = high) and nibble value v, the 32-byte row
+     * (S_i contribution, i = 0..31) is split in two 16-byte planes h:
+     *   synt[((m*2 + n)*2 + h)*16 + v]  = bytes i = 16h .. 16h+15 of
+     *   (v << 4n) * beta_i^-(m+1)   (see RsCorrParams for beta_i).
+     * Plane-major layout keeps the 16 rows of a plane in 16 distinct LDS
+     * bank slots. */
+    uint4 synt[32 * 2 * 2 * 16];
+    /* chien[(j-1)*255 + e] = 16 bytes alpha^(e + j*b), b = 0..15: the j-th
+     * locator term at 16 consecutive points for a coefficient of log e. */
+    uint4 chien[16 * 255];
 };
 
 /*
@@ -41,6 +52,7 @@ struct RsCorrParams {
     uint32_t fcr, prim, iprim;
     uint32_t size;   /* message bytes per codeword (1..223) */
     int32_t pad;     /* 255 - 32 - size */
+    uint32_t vfast;  /* (fcr+31)*prim*254 < 32768: verification exponents need no int16 emulation */
     uint8_t tr_start[RS_NR];
     uint8_t tr_inc[RS_NR];
 };
@@ -53,24 +65,25 @@ extern "C" {
 hipError_t rsk_encode(const RsDevTables *tab, const uint8_t *data, size_t dstride, uint8_t *parity, size_t pstride,
                       uint32_t size, size_t count, int num_cu, hipStream_t stream);
 
-/* remainder of (data || parity) mod g, 32 bytes per codeword into rem */
-hipError_t rsk_remainder(const RsDevTables *tab, const uint8_t *data, size_t dstride, const uint8_t *parity,
-                         size_t pstride, uint32_t size, size_t count, uint8_t *rem, int num_cu, hipStream_t stream);
+/* 32 syndromes (poly form, S_i = c(beta_i)) per codeword into syn, via the
+ * remainder of (data || parity) * x^32 mod g and the synt transform */
+hipError_t rsk_syndrome(const RsDevTables *tab, const uint8_t *data, size_t dstride, const uint8_t *parity,
+                        size_t pstride, uint32_t size, size_t count, uint8_t *syn, int num_cu, hipStream_t stream);
 
 /* flag[c] = remainder of codeword c is nonzero */
 hipError_t rsk_check(const RsDevTables *tab, const uint8_t *data, size_t dstride, const uint8_t *parity, size_t pstride,
                      uint32_t size, size_t count, uint8_t *flag, int num_cu, hipStream_t stream);
 
 /*
- * Correction.  Exactly one of rem / ext_syn is non-NULL (ext_syn: 32 log-form
- * syndromes per codeword, the config's "syndrome" pointer path).  pos8 / pos32
- * (at most one non-NULL) select erasure mode with per-codeword slot arrays of
- * pos_stride entries and counts in cnt.
+ * Correction.  syn: 32 syndromes per codeword, poly form (from rsk_syndrome)
+ * or, with syn_is_log, log form (the config's external "syndrome" pointer
+ * path).  pos8 / pos32 (at most one non-NULL) select erasure mode with
+ * per-codeword slot arrays of pos_stride entries and counts in cnt.
  */
 hipError_t rsk_correct(const RsDevTables *tab, const RsCorrParams *prm, uint8_t *data, size_t dstride, uint8_t *parity,
-                       size_t pstride, size_t count, const uint8_t *rem, const uint8_t *ext_syn, const uint8_t *pos8,
+                       size_t pstride, size_t count, const uint8_t *syn, int syn_is_log, const uint8_t *pos8,
                        const uint32_t *pos32, size_t pos_stride, const uint8_t *cnt, uint8_t *ok, uint8_t *corrected,
-                       hipStream_t stream);
+                       int num_cu, hipStream_t stream);
 
 #ifdef __cplusplus
 }

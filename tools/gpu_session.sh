@@ -28,6 +28,17 @@ for step in "$@"; do
     bench) run bench 600 python bench.py ;;
     prof) run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- \
         python3 bench.py --no-cpu-baseline --steps 10 ;;
+    pmc)
+        # one rocprofv3 pass per counter group (never combined with tracing)
+        i=0
+        for grp in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE" \
+                   "SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAIT_ANY" \
+                   "SQ_INSTS_SMEM SQ_INSTS_BRANCH SQ_IFETCH SQ_ACTIVE_INST_LDS SQ_INST_CYCLES_SALU" \
+                   "FETCH_SIZE" "WRITE_SIZE"; do
+            run pmc$i 300 rocprofv3 --pmc $grp -d gpurun_out/pmc$i -o pmc --output-format csv -- \
+                python3 tools/kernel_driver.py --reps 3
+            i=$((i+1))
+        done ;;
     *) echo "unknown step $step"; exit 2 ;;
     esac
 done

@@ -1,0 +1,56 @@
+#!/usr/bin/env python3
+"""Minimal driver for profiling: REPS x (encode, inject, decode) on N codewords
+through the C ABI, nothing else (no CPU baseline, no extra passes).  Used under
+rocprofv3 by tools/gpu_session.sh (steps prof / pmc).
+
+    python tools/kernel_driver.py [--n 1048576] [--reps 5] [--mode roundtrip|erasure]
+"""
+import argparse
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+
+import bench  # noqa: E402
+import libpoporon_amd as P  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--n", type=int, default=1 << 20)
+    ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--mode", default="roundtrip", choices=["roundtrip", "erasure"])
+    a = ap.parse_args()
+    dev = torch.device("cuda", 0)
+    rs = P.Poporon.default(device=0)
+    rs.reserve(a.n)
+    K, N = 223, 255
+    cw = torch.zeros((a.n, N), dtype=torch.uint8, device=dev)
+    cw[:, :K] = bench.synth_bytes(bench.SEED, 0, a.n, K, dev)
+    ok = torch.zeros(a.n, dtype=torch.uint8, device=dev)
+    cor = torch.zeros(a.n, dtype=torch.uint8, device=dev)
+    s = torch.cuda.current_stream().cuda_stream
+    b = cw.data_ptr()
+    if a.mode == "roundtrip":
+        pos, mag = bench.synth_errors(bench.SEED + 1, 0, a.n, 16, N, dev)
+        kw = {}
+    else:
+        pos, mag = bench.synth_errors(bench.SEED + 2, 0, a.n, 32, K, dev)
+        pos = pos.sort(dim=1).values
+        slots = pos.to(torch.uint8).contiguous()
+        cnt = torch.full((a.n,), 32, dtype=torch.uint8, device=dev)
+        kw = dict(d_positions=slots.data_ptr(), positions_stride=32, d_counts=cnt.data_ptr())
+    for _ in range(a.reps):
+        rs.encode_batch_device(b, N, b + K, N, K, a.n, s)
+        cw.scatter_(1, pos, cw.gather(1, pos) ^ mag)
+        rs.decode_batch_device(b, N, b + K, N, K, a.n, ok.data_ptr(), cor.data_ptr(), stream=s, **kw)
+    torch.cuda.synchronize()
+    assert int(ok.sum()) == a.n, "decode failures"
+    print("driver ok", a.mode, a.n, a.reps)
+
+
+if __name__ == "__main__":
+    main()
