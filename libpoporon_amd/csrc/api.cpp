@@ -433,13 +433,15 @@ static void build_tables(poporon_t *h)
     }
     /* Chien chunk rows: term j at 16 consecutive points */
     for (uint32_t j = 1; j <= 16; j++) {
-        for (uint32_t e = 0; e < 255; e++) {
+        for (uint32_t e = 0; e < 256; e++) {
             uint8_t rowb[16];
             for (uint32_t b = 0; b < 16; b++)
-                rowb[b] = (uint8_t)gf->log2exp[(e + j * b) % 255];
-            memcpy(&t.chien[(j - 1) * 255 + e], rowb, 16);
+                rowb[b] = e == 255 ? 0 : (uint8_t)gf->log2exp[(e + j * b) % 255];
+            memcpy(&t.chien[(j - 1) * 256 + e], rowb, 16);
         }
     }
+    const char *fv = getenv("POPORON_AMD_FORCE_VERIFY");
+    p.force_verify = (fv && fv[0] == '1') ? 1u : 0u;
 }
 
 static bool params_supported(const poporon_t *h)

@@ -37,9 +37,10 @@ struct RsDevTables {
      * Plane-major layout keeps the 16 rows of a plane in 16 distinct LDS
      * bank slots. */
     uint4 synt[32 * 2 * 2 * 16];
-    /* chien[(j-1)*255 + e] = 16 bytes alpha^(e + j*b), b = 0..15: the j-th
-     * locator term at 16 consecutive points for a coefficient of log e. */
-    uint4 chien[16 * 255];
+    /* chien[(j-1)*256 + e] = 16 bytes alpha^(e + j*b), b = 0..15: the j-th
+     * locator term at 16 consecutive points for a coefficient of log e;
+     * entry e = 255 (log of zero) is an all-zero row. */
+    uint4 chien[16 * 256];
 };
 
 /*
@@ -53,6 +54,7 @@ struct RsCorrParams {
     uint32_t size;   /* message bytes per codeword (1..223) */
     int32_t pad;     /* 255 - 32 - size */
     uint32_t vfast;  /* (fcr+31)*prim*254 < 32768: verification exponents need no int16 emulation */
+    uint32_t force_verify; /* run the re-syndrome check even where it provably passes (tests) */
     uint8_t tr_start[RS_NR];
     uint8_t tr_inc[RS_NR];
 };
