@@ -442,6 +442,8 @@ static void build_tables(poporon_t *h)
     }
     const char *fv = getenv("POPORON_AMD_FORCE_VERIFY");
     p.force_verify = (fv && fv[0] == '1') ? 1u : 0u;
+    const char *sa = getenv("POPORON_AMD_STOP_AT"); /* profiling ablation only */
+    p.stop_at = sa ? (uint32_t)atoi(sa) : 0u;
 }
 
 static bool params_supported(const poporon_t *h)

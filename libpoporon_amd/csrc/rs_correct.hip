@@ -201,6 +201,9 @@ __device__ __forceinline__ bool correct_one(const Gf &gf, const uint4 *__restric
         }
     }
 
+    if (P.stop_at == 2u)
+        return dl > 40u; /* profiling ablation */
+
     /* ---- log form and degree, src/decode.c:98-110 ---- */
     uint32_t ll[RS_NR + 1];
     uint32_t deg = 0;
@@ -213,9 +216,16 @@ __device__ __forceinline__ bool correct_one(const Gf &gf, const uint4 *__restric
         return false;
     const uint32_t degmax = wave_max(deg);
 
-    /* ---- Chien search: root map over the 255 points ---- */
+    /* ---- Chien search: root map over the 255 points ----
+     * With num_roots erasures BM does not run (src/decode.c:55) and Lambda is
+     * exactly prod(1 + X_l x): its roots are the points alpha^i with
+     * i = -log X_l, so the map is built from the positions (a repeated X_l is
+     * a double root that the search counts once: cnt < deg fails below, as in
+     * the reference).  Other lanes search. */
+    const bool direct = ne == RS_NR;
+    const uint32_t degsearch = wave_max(direct ? 0u : deg);
     uint32_t rb[8];
-    if (degmax <= 16) {
+    if (degsearch <= 16) {
         /* chunk a: points i' = 16a + b: Lambda = 1 + sum_j T_j[e_j], e_j = log(Lambda_j) + 16aj */
         uint32_t ej[17];
 #pragma unroll
@@ -226,7 +236,7 @@ __device__ __forceinline__ bool correct_one(const Gf &gf, const uint4 *__restric
             uint32_t acc[4] = {0x01010101u, 0x01010101u, 0x01010101u, 0x01010101u};
 #pragma unroll
             for (int j = 1; j <= 16; ++j) {
-                if ((uint32_t)j <= degmax) {
+                if ((uint32_t)j <= degsearch) {
                     const uint4 row = chien[(j - 1) * 256 + ej[j]];
                     acc[0] ^= row.x;
                     acc[1] ^= row.y;
@@ -272,12 +282,29 @@ __device__ __forceinline__ bool correct_one(const Gf &gf, const uint4 *__restric
             acc ^= (reg[j] != A0) ? gf.exp(red(reg[j] + j)) : 0u;
         rb[0] |= (acc == 0 ? 1u : 0u);
     }
+    if (wave_max(direct ? 1u : 0u)) {
+        uint32_t dm[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        if (direct) {
+            for (uint32_t l = 0; l < RS_NR; ++l) {
+                const uint32_t xl = mod255(P.prim * (uint32_t)(RS_NN - 1u - ((uint32_t)pos[l] + (uint32_t)pad)));
+                const uint32_t ip = xl ? RS_NN - xl : 0u; /* i' = -log X_l mod 255 */
+#pragma unroll
+                for (int w = 0; w < 8; ++w)
+                    dm[w] |= ((ip >> 5) == (uint32_t)w) ? (1u << (ip & 31u)) : 0u;
+            }
+        }
+#pragma unroll
+        for (int w = 0; w < 8; ++w)
+            rb[w] = direct ? dm[w] : rb[w];
+    }
     uint32_t cnt = 0;
 #pragma unroll
     for (int w = 0; w < 8; ++w)
         cnt += __popc(rb[w]);
     if (cnt != deg)
         return false; /* src/decode.c:143-145 */
+    if (P.stop_at == 3u)
+        return false; /* profiling ablation */
 
     /* locations k = (i*iprim - 1) mod 255 below pad fail, src/decode.c:132-134 */
     if (pad > 0) {
@@ -308,6 +335,8 @@ __device__ __forceinline__ bool correct_one(const Gf &gf, const uint4 *__restric
             om[m] = ((uint32_t)m < deg) ? gf.log(acc) : A0;
         }
     }
+    if (P.stop_at == 4u)
+        return (om[0] ^ om[1]) > 300u; /* profiling ablation */
     const uint32_t dtop = (deg < RS_NR - 1 ? deg : RS_NR - 1) & ~1u;
     const uint32_t dtopmax = wave_max(dtop);
     const uint32_t cntmax = wave_max(cnt);
@@ -445,7 +474,7 @@ __global__ __launch_bounds__(COR_WG) void rs_correct_k(const RsDevTables *__rest
         const uint32_t ne = pos ? cnt[cw] : 0u;
         if (ne > RS_NR)
             good = false; /* undefined behaviour in the reference (quirk Q5): refused */
-        else if (any)
+        else if (any && P.stop_at != 1u)
             good = correct_one<PosT>(gf, lch, srow, P, data + cw * dstride, parity + cw * pstride, ne,
                                      pos ? pos + cw * pos_stride : nullptr, fixed);
         ok[cw] = good ? 1 : 0;

@@ -104,9 +104,102 @@ __device__ __forceinline__ void lfsr_feed(uint32_t (&P)[8], const uint8_t *p, ui
     }
 }
 
+/* Fixed-length stream of N message bytes at any alignment: all the 16-byte
+ * aligned chunks that hold message bytes are loaded up front (dwordx4, one
+ * request per 16 B, everything in flight at once), then message dwords are
+ * re-aligned in registers: dword k = bytes [4k, 4k+4) = funnel of stream
+ * dwords q = k + sh/4 and q+1 by sh%4 bytes, with the per-lane q offset
+ * resolved by a 2-level select (no dynamic register indexing). */
+template <int N>
+struct Stream {
+    static constexpr int NCH = (N + 30) / 16; /* chunks covering up to 15 + N bytes */
+    uint32_t D[NCH * 4 + 4];
+    uint32_t sdw, sb;
+    __device__ __forceinline__ void load(const uint8_t *p)
+    {
+        const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+        const uint4 *c16 = reinterpret_cast<const uint4 *>(a & ~uintptr_t(15));
+        const uint32_t sh = static_cast<uint32_t>(a & 15u);
+        sdw = sh >> 2;
+        sb = sh & 3u;
+#pragma unroll
+        for (int c = 0; c < NCH; ++c) {
+            uint4 v = make_uint4(0, 0, 0, 0);
+            if ((uint32_t)(16 * c) < sh + (uint32_t)N) /* chunk holds a message byte: same page */
+                v = c16[c];
+            D[4 * c] = v.x;
+            D[4 * c + 1] = v.y;
+            D[4 * c + 2] = v.z;
+            D[4 * c + 3] = v.w;
+        }
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+            D[NCH * 4 + t] = 0;
+    }
+    __device__ __forceinline__ uint32_t at(int q) const /* stream dword q + sdw */
+    {
+        const uint32_t t0 = (sdw & 1u) ? D[q + 1] : D[q];
+        const uint32_t t1 = (sdw & 1u) ? D[q + 3] : D[q + 2];
+        return (sdw & 2u) ? t1 : t0;
+    }
+    __device__ __forceinline__ uint32_t word(int k) const /* message dword k */
+    {
+        return __builtin_amdgcn_alignbyte(at(k + 1), at(k), sb);
+    }
+};
+
+template <int N>
+__device__ __forceinline__ void lfsr_stream(uint32_t (&P)[8], const Stream<N> &s, const uint4 *__restrict__ tab)
+{
+#pragma unroll
+    for (int k = 0; k < N / 4; ++k)
+        lfsr_word(P, s.word(k), tab);
+    if (N % 4) {
+        const uint32_t w = s.word(N / 4);
+#pragma unroll
+        for (int b = 0; b < N % 4; ++b)
+            lfsr_step(P, (w >> (8 * b)) & 0xffu, tab);
+    }
+}
+
+/* Store the 32-byte register at any alignment without touching neighbours:
+ * up to 3 leading bytes, aligned dwords, up to 3 trailing bytes. */
+__device__ __forceinline__ void store32_any(uint8_t *o, const uint32_t (&P)[8])
+{
+    const uint32_t lead = (uint32_t)((4u - (reinterpret_cast<uintptr_t>(o) & 3u)) & 3u);
+    const uint32_t X[9] = {P[0], P[1], P[2], P[3], P[4], P[5], P[6], P[7], 0u};
+    if (lead == 0u) {
+        uint32_t *o4 = reinterpret_cast<uint32_t *>(o);
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+            o4[k] = P[k];
+        return;
+    }
+    /* bytes 0 .. lead-1 */
+    o[0] = (uint8_t)P[0];
+    if (lead > 1u)
+        o[1] = (uint8_t)(P[0] >> 8);
+    if (lead > 2u)
+        o[2] = (uint8_t)(P[0] >> 16);
+    /* 7 aligned dwords: bytes lead + 4j .. lead + 4j + 3 */
+    uint32_t *o4 = reinterpret_cast<uint32_t *>(o + lead);
+#pragma unroll
+    for (int j = 0; j < 7; ++j)
+        o4[j] = __builtin_amdgcn_alignbyte(X[j + 1], X[j], lead);
+    /* bytes lead + 28 .. 31 */
+    const uint32_t t = __builtin_amdgcn_alignbyte(X[8], X[7], lead);
+    uint8_t *ot = o + lead + 28;
+    ot[0] = (uint8_t)t;
+    if (lead < 3u)
+        ot[1] = (uint8_t)(t >> 8);
+    if (lead < 2u)
+        ot[2] = (uint8_t)(t >> 16);
+}
+
 #define MODE_ENCODE 0
 #define MODE_SYNDROME 1
 #define MODE_CHECK 2
+#define FULL_K 223 /* message length of the full-length RS(255,223) code: fixed-stream path */
 
 template <int MODE>
 __global__ __launch_bounds__(LFSR_WG) void rs_lfsr_k(const RsDevTables *__restrict__ T,
@@ -126,9 +219,23 @@ __global__ __launch_bounds__(LFSR_WG) void rs_lfsr_k(const RsDevTables *__restri
 
     for (size_t cw = (size_t)blockIdx.x * LFSR_WG + threadIdx.x; cw < count; cw += (size_t)gridDim.x * LFSR_WG) {
         uint32_t P[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-        lfsr_feed(P, data + cw * dstride, size, tab);
+        if (size == FULL_K) { /* uniform: fixed-length streams, all loads in flight up front */
+            Stream<FULL_K> sd;
+            sd.load(data + cw * dstride);
+            if (MODE != MODE_ENCODE) {
+                Stream<RS_NR> sp;
+                sp.load(parity + cw * pstride);
+                lfsr_stream(P, sd, tab);
+                lfsr_stream(P, sp, tab);
+            } else {
+                lfsr_stream(P, sd, tab);
+            }
+        } else {
+            lfsr_feed(P, data + cw * dstride, size, tab);
+            if (MODE != MODE_ENCODE)
+                lfsr_feed(P, parity + cw * pstride, RS_NR, tab);
+        }
         if (MODE == MODE_SYNDROME) {
-            lfsr_feed(P, parity + cw * pstride, RS_NR, tab);
             /* S = sum over remainder bytes m of T_m,lo[r_m & 15] ^ T_m,hi[r_m >> 4] */
             uint32_t S[8] = {0, 0, 0, 0, 0, 0, 0, 0};
             if ((P[0] | P[1] | P[2] | P[3] | P[4] | P[5] | P[6] | P[7]) != 0u) {
@@ -152,20 +259,10 @@ __global__ __launch_bounds__(LFSR_WG) void rs_lfsr_k(const RsDevTables *__restri
             o[0] = make_uint4(S[0], S[1], S[2], S[3]);
             o[1] = make_uint4(S[4], S[5], S[6], S[7]);
         } else if (MODE == MODE_CHECK) {
-            lfsr_feed(P, parity + cw * pstride, RS_NR, tab);
             out[cw] = (P[0] | P[1] | P[2] | P[3] | P[4] | P[5] | P[6] | P[7]) != 0u;
         } else {
-            uint8_t *o = parity + cw * pstride;
-            if (par_aligned) {
-                uint32_t *o4 = reinterpret_cast<uint32_t *>(o);
-#pragma unroll
-                for (int k = 0; k < 8; ++k)
-                    o4[k] = P[k];
-            } else {
-#pragma unroll
-                for (int k = 0; k < 32; ++k)
-                    o[k] = (uint8_t)(P[k >> 2] >> (8 * (k & 3)));
-            }
+            (void)par_aligned;
+            store32_any(parity + cw * pstride, P);
         }
     }
 }
