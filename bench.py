@@ -110,8 +110,9 @@ def barrier(world):
     torch.cuda.synchronize()
 
 
-def allreduce(x, op, world):
-    t = torch.tensor([x], dtype=torch.float64, device="cuda")
+def allreduce(x, op, world, device="cuda"):
+    """Scalar reduction over ranks (RCCL on GPU, gloo on CPU in the tests)."""
+    t = torch.tensor([x], dtype=torch.float64, device=device)
     if world > 1:
         dist.all_reduce(t, op=op)
     return float(t.item())
