@@ -6,7 +6,7 @@ resident in HBM (configs[1] + configs[2] of BASELINE.json, chained):
 
     encode  2^20 messages x 223 B -> 32 parity bytes each        (HIP, C ABI)
     inject  16 errors per codeword (fixed pattern: unique positions over all
-            255 bytes, magnitudes in [1,255])                   (torch scatter)
+            255 bytes, magnitudes in [1,255])   (channel kernel, csrc/channel.hip)
     decode  remainder + syndromes/BM/Chien/Forney/apply, in place (HIP, C ABI)
 
 The decode undoes the injection, so every step sees the same workload and
@@ -215,13 +215,14 @@ def main():
     cw = torch.zeros((B, N), dtype=torch.uint8, device=dev)
     cw[:, :K] = synth_bytes(SEED, first, B, K, dev)
     pos, mag = synth_errors(SEED + 1, first, B, 16, N, dev)
+    pos8, mag8 = pos.to(torch.uint8).contiguous(), mag.to(torch.uint8).contiguous()
     okb = torch.zeros(B, dtype=torch.uint8, device=dev)
     corb = torch.zeros(B, dtype=torch.uint8, device=dev)
     base = cw.data_ptr()
 
     def step():
         rs.encode_batch_device(base, N, base + K, N, K, B, stream)
-        cw.scatter_(1, pos, cw.gather(1, pos) ^ mag)
+        P.channel_xor_device(pos8.data_ptr(), mag8.data_ptr(), 16, base, N, B, stream)
         rs.decode_batch_device(base, N, base + K, N, K, B, okb.data_ptr(), corb.data_ptr(), stream=stream)
 
     for _ in range(args.warmup):
@@ -272,13 +273,14 @@ def main():
     erasure = None
     if not args.no_erasure:
         epos, emag = synth_errors(SEED + 2, first, B, 32, K, dev)
-        epos = epos.sort(dim=1).values
+        epos, order = epos.sort(dim=1)
         slots = epos.to(torch.uint8).contiguous()
+        emag8 = emag.gather(1, order).to(torch.uint8).contiguous()
         cnts = torch.full((B,), 32, dtype=torch.uint8, device=dev)
         rs.encode_batch_device(base, N, base + K, N, K, B, stream)
 
         def estep():
-            cw.scatter_(1, epos, cw.gather(1, epos) ^ emag)
+            P.channel_xor_device(slots.data_ptr(), emag8.data_ptr(), 32, base, N, B, stream)
             rs.decode_batch_device(base, N, base + K, N, K, B, okb.data_ptr(), corb.data_ptr(),
                                    d_positions=slots.data_ptr(), positions_stride=32, d_counts=cnts.data_ptr(),
                                    stream=stream)

@@ -100,6 +100,14 @@ bool poporon_decode_batch(poporon_t *pprn, uint8_t *data, size_t data_stride, ui
 bool poporon_amd_timing(poporon_t *pprn, int enable);
 bool poporon_amd_timing_read(poporon_t *pprn, int kernel, double *total_ms, uint64_t *launches);
 
+/* ---- test / benchmark utility (not part of the codec) ---------------------
+ * Symbol-error channel: for each of count codeword rows (stride bytes apart)
+ * XOR d_magnitudes[c*per_codeword + e] into byte d_positions[c*per_codeword + e]
+ * of row c, in place, asynchronously on stream.  Positions within a row must
+ * be distinct. */
+bool poporon_amd_channel_xor_device(const uint8_t *d_positions, const uint8_t *d_magnitudes, size_t per_codeword,
+                                    uint8_t *d_codewords, size_t stride, size_t count, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -82,6 +82,7 @@ _SIGS = {
     "poporon_encode_batch": (C.c_bool, [_vp, _vp, C.c_size_t, _vp, C.c_size_t, C.c_size_t, C.c_size_t]),
     "poporon_decode_batch": (C.c_bool, [_vp, _vp, C.c_size_t, _vp, C.c_size_t, C.c_size_t, C.c_size_t, _vp,
                                         C.c_size_t, _vp, _vp, _vp]),
+    "poporon_amd_channel_xor_device": (C.c_bool, [_vp, _vp, C.c_size_t, _vp, C.c_size_t, C.c_size_t, _vp]),
 }
 
 # kernel ids for poporon_amd_timing_read (include/poporon_amd.h)
@@ -319,6 +320,13 @@ class Poporon:
         n = C.c_uint64(0)
         self._check(self.lib.poporon_amd_timing_read(self.h, kernel, C.byref(ms), C.byref(n)), "poporon_amd_timing_read")
         return ms.value, n.value
+
+
+def channel_xor_device(d_positions, d_magnitudes, per_codeword, d_codewords, stride, count, stream=0):
+    """Test/benchmark channel: XOR magnitudes into positions of each codeword row (device pointers, async)."""
+    if not load_library().poporon_amd_channel_xor_device(d_positions, d_magnitudes, per_codeword, d_codewords,
+                                                         stride, count, stream or None):
+        raise PoporonError(f"poporon_amd_channel_xor_device failed: {last_error()}")
 
 
 def shard_range(count: int, rank: int, world: int):

@@ -392,11 +392,16 @@ static void build_tables(poporon_t *h)
         for (uint32_t m = 0; m < 32; m++)
             row[m] = fb == 0 ? 0
                              : (uint8_t)gf->log2exp[gf_mod(gf, (uint16_t)(gf->exp2log[fb] + g[RS_NR - 1 - m]))];
-        memcpy(&t.lfsr[fb * 2], row, 16);
-        memcpy(&t.lfsr[fb * 2 + 1], row + 16, 16);
+        uint32_t il[8]; /* interleaved: dword k = row bytes k, k+8, k+16, k+24 */
+        for (uint32_t k = 0; k < 8; k++)
+            il[k] = (uint32_t)row[k] | ((uint32_t)row[k + 8] << 8) | ((uint32_t)row[k + 16] << 16) |
+                    ((uint32_t)row[k + 24] << 24);
+        memcpy(&t.lfsr[fb * 2], il, 16);
+        memcpy(&t.lfsr[fb * 2 + 1], il + 4, 16);
     }
     for (uint32_t x = 0; x < 512; x++)
         t.exp2[x] = (uint8_t)gf->log2exp[x % 255];
+    t.exp2[511] = 0; /* ZLOG sentinel of the correction kernel (no sum of two logs reaches 511) */
     for (uint32_t v = 0; v < 256; v++)
         t.log[v] = (uint8_t)gf->exp2log[v];
 

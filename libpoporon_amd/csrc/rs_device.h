@@ -16,13 +16,16 @@
 
 /*
  * Device-resident per-handle tables (one hipMalloc, built on the host by
- * rs_tables.cpp from the handle's GF tables and generator polynomial).
+ * api.cpp from the handle's GF tables and generator polynomial).
  *
  *  lfsr[fb*2 + h]  : 16-byte half h of the 32-byte LFSR row for feedback byte
- *                    fb: byte m = alpha^(log fb + g[31-m]) with the
+ *                    fb: row byte m = alpha^(log fb + g[31-m]) with the
  *                    reference's gf_mod semantics (src/encode.c:126-140), so
- *                    that  P' = (P >> 8 bits) ^ row[fb]  is one encode step.
- *  exp2[x]         : alpha^(x mod 255) for x < 512 (exp2[255] = 1).
+ *                    that  p'_m = p_m+1 ^ row_m  is one encode step; stored
+ *                    interleaved, dword k = row bytes (k, k+8, k+16, k+24)
+ *                    (the register layout of rs_kernels.hip).
+ *  exp2[x]         : alpha^(x mod 255) for x < 511 (exp2[255] = 1); exp2[511] = 0
+ *                    (log-of-zero sentinel of the correction kernel).
  *  log[v]          : discrete log, log[0] = 255.
  */
 struct RsDevTables {

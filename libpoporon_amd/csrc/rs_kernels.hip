@@ -41,33 +41,97 @@
 /* LFSR (encode / syndromes / check)                                        */
 /* ------------------------------------------------------------------------ */
 
-__device__ __forceinline__ void lfsr_step(uint32_t (&P)[8], uint32_t in_byte, const uint4 *__restrict__ tab)
+/*
+ * Interleaved shift register.  The 32 register bytes p_0..p_31 (p_0 = the
+ * highest-degree remainder coefficient, the next feedback) are kept as 8
+ * dwords, logical dword k = bytes (p_k, p_k+8, p_k+16, p_k+24), and logical
+ * dword k lives in X[(k + r) & 7] after r steps.  One step
+ *     fb = p_0 ^ d;  p'_j = p_j+1 ^ row[fb]_j;  p'_31 = row[fb]_31
+ * is then a renaming of the dwords (logical k+1 becomes k) plus one 8-bit
+ * shift of the dword that wraps around (logical 0 -> 7), and the row table
+ * (T->lfsr) stores rows in the same interleaved order.  Two steps' row XORs
+ * fuse into one v_bitop3_b32 (3-way XOR) per dword; only the dword that feeds the next
+ * step is brought up to date eagerly.  With the rotation r a compile-time
+ * constant (fully unrolled loops) a step costs ~8 VALU + 2 ds_read_b128,
+ * against ~20 VALU for a funnel-shifted register.
+ */
+__device__ __forceinline__ void il_rows(uint32_t (&R)[8], uint32_t fb, const uint4 *__restrict__ tab)
 {
-    const uint32_t fb = (P[0] ^ in_byte) & 0xffu;
     const uint4 a = tab[fb * (2 * LFSR_REPL)];
     const uint4 b = tab[fb * (2 * LFSR_REPL) + LFSR_REPL];
-    P[0] = __builtin_amdgcn_alignbyte(P[1], P[0], 1) ^ a.x;
-    P[1] = __builtin_amdgcn_alignbyte(P[2], P[1], 1) ^ a.y;
-    P[2] = __builtin_amdgcn_alignbyte(P[3], P[2], 1) ^ a.z;
-    P[3] = __builtin_amdgcn_alignbyte(P[4], P[3], 1) ^ a.w;
-    P[4] = __builtin_amdgcn_alignbyte(P[5], P[4], 1) ^ b.x;
-    P[5] = __builtin_amdgcn_alignbyte(P[6], P[5], 1) ^ b.y;
-    P[6] = __builtin_amdgcn_alignbyte(P[7], P[6], 1) ^ b.z;
-    P[7] = (P[7] >> 8) ^ b.w;
+    R[0] = a.x, R[1] = a.y, R[2] = a.z, R[3] = a.w;
+    R[4] = b.x, R[5] = b.y, R[6] = b.z, R[7] = b.w;
 }
 
-__device__ __forceinline__ void lfsr_word(uint32_t (&P)[8], uint32_t w, const uint4 *__restrict__ tab)
+/* a ^ b ^ c in one VALU op (gfx950 v_bitop3_b32, truth table 0x96) */
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c)
 {
-    lfsr_step(P, w & 0xffu, tab);
-    lfsr_step(P, (w >> 8) & 0xffu, tab);
-    lfsr_step(P, (w >> 16) & 0xffu, tab);
-    lfsr_step(P, w >> 24, tab);
+    return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
 }
 
-/* Feed n bytes starting at p (any alignment).  Only aligned dwords that
- * contain at least one message byte are loaded, so no load can cross into an
- * unmapped page. */
-__device__ __forceinline__ void lfsr_feed(uint32_t (&P)[8], const uint8_t *p, uint32_t n, const uint4 *__restrict__ tab)
+/* one step at rotation r; d holds the input byte in bits 0..7 (upper bits ignored) */
+__device__ __forceinline__ void il_step(uint32_t (&X)[8], int r, uint32_t d, const uint4 *__restrict__ tab)
+{
+    uint32_t R[8];
+    il_rows(R, (X[r & 7] ^ d) & 0xffu, tab);
+    X[r & 7] = (X[r & 7] >> 8) ^ R[7];
+#pragma unroll
+    for (int k = 0; k < 7; ++k)
+        X[(r + 1 + k) & 7] ^= R[k];
+}
+
+/* two steps at rotation r, r+1 */
+__device__ __forceinline__ void il_pair(uint32_t (&X)[8], int r, uint32_t d0, uint32_t d1,
+                                        const uint4 *__restrict__ tab)
+{
+    uint32_t Ra[8], Rb[8];
+    const int i0 = r & 7, i1 = (r + 1) & 7;
+    il_rows(Ra, (X[i0] ^ d0) & 0xffu, tab);
+    X[i1] ^= Ra[0]; /* next logical 0: needed now */
+    const uint32_t w = X[i0] >> 8;
+    il_rows(Rb, (X[i1] ^ d1) & 0xffu, tab);
+#pragma unroll
+    for (int j = 1; j < 7; ++j)
+        X[(r + 1 + j) & 7] = xor3(X[(r + 1 + j) & 7], Ra[j], Rb[j - 1]);
+    X[i0] = xor3(w, Ra[7], Rb[6]);
+    X[i1] = (X[i1] >> 8) ^ Rb[7];
+}
+
+/* X[(k + r) & 7] -> X[k], r uniform at run time */
+__device__ __forceinline__ void il_normalize(uint32_t (&X)[8], uint32_t r)
+{
+#pragma unroll
+    for (int s = 1; s < 8; s <<= 1) {
+        const bool c = (r & (uint32_t)s) != 0u;
+        uint32_t T[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+            T[k] = c ? X[(k + s) & 7] : X[k];
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+            X[k] = T[k];
+    }
+}
+
+/* register byte m (0 = highest degree) at rotation r */
+__device__ __forceinline__ uint32_t il_byte(const uint32_t (&X)[8], int r, int m)
+{
+    return (X[(m + r) & 7] >> (8 * (m >> 3))) & 0xffu;
+}
+
+/* the 32 register bytes in order, as 8 dwords (byte m of the register = byte m & 3 of dword m >> 2) */
+__device__ __forceinline__ void il_bytes(uint32_t (&P)[8], const uint32_t (&X)[8], int r)
+{
+#pragma unroll
+    for (int q = 0; q < 8; ++q)
+        P[q] = il_byte(X, r, 4 * q) | (il_byte(X, r, 4 * q + 1) << 8) | (il_byte(X, r, 4 * q + 2) << 16) |
+               (il_byte(X, r, 4 * q + 3) << 24);
+}
+
+/* Feed n bytes starting at p (any alignment), rotation 0 on entry and on
+ * exit.  Only aligned dwords that contain at least one message byte are
+ * loaded, so no load can cross into an unmapped page. */
+__device__ __forceinline__ void lfsr_feed(uint32_t (&X)[8], const uint8_t *p, uint32_t n, const uint4 *__restrict__ tab)
 {
     const uintptr_t a = reinterpret_cast<uintptr_t>(p);
     const uint32_t *w = reinterpret_cast<const uint32_t *>(a & ~uintptr_t(3));
@@ -78,15 +142,16 @@ __device__ __forceinline__ void lfsr_feed(uint32_t (&P)[8], const uint8_t *p, ui
     uint32_t cur = w[0];
     uint32_t q = 0;
     uint32_t i = 0;
-    for (; i + 16u <= n; i += 16u, q += 4u) {
+    for (; i + 16u <= n; i += 16u, q += 4u) { /* 16 steps: the rotation comes back to 0 */
         const uint32_t w1 = (q + 1u < nd) ? w[q + 1u] : 0u;
         const uint32_t w2 = (q + 2u < nd) ? w[q + 2u] : 0u;
         const uint32_t w3 = (q + 3u < nd) ? w[q + 3u] : 0u;
         const uint32_t w4 = (q + 4u < nd) ? w[q + 4u] : 0u;
-        lfsr_word(P, __builtin_amdgcn_alignbyte(w1, cur, sh), tab);
-        lfsr_word(P, __builtin_amdgcn_alignbyte(w2, w1, sh), tab);
-        lfsr_word(P, __builtin_amdgcn_alignbyte(w3, w2, sh), tab);
-        lfsr_word(P, __builtin_amdgcn_alignbyte(w4, w3, sh), tab);
+        const uint32_t m[4] = {__builtin_amdgcn_alignbyte(w1, cur, sh), __builtin_amdgcn_alignbyte(w2, w1, sh),
+                               __builtin_amdgcn_alignbyte(w3, w2, sh), __builtin_amdgcn_alignbyte(w4, w3, sh)};
+#pragma unroll
+        for (int b = 0; b < 16; b += 2)
+            il_pair(X, b, m[b >> 2] >> (8 * (b & 3)), m[(b + 1) >> 2] >> (8 * ((b + 1) & 3)), tab);
         cur = w4;
     }
     if (i < n) {
@@ -96,11 +161,15 @@ __device__ __forceinline__ void lfsr_feed(uint32_t (&P)[8], const uint8_t *p, ui
         const uint32_t w4 = (q + 4u < nd) ? w[q + 4u] : 0u;
         const uint32_t m[4] = {__builtin_amdgcn_alignbyte(w1, cur, sh), __builtin_amdgcn_alignbyte(w2, w1, sh),
                                __builtin_amdgcn_alignbyte(w3, w2, sh), __builtin_amdgcn_alignbyte(w4, w3, sh)};
-        const uint32_t left = n - i;
+        const uint32_t left = n - i; /* uniform */
 #pragma unroll
-        for (uint32_t b = 0; b < 16u; ++b)
-            if (b < left)
-                lfsr_step(P, (m[b >> 2] >> (8u * (b & 3u))) & 0xffu, tab);
+        for (int b = 0; b < 16; b += 2) {
+            if ((uint32_t)b + 1u < left)
+                il_pair(X, b, m[b >> 2] >> (8 * (b & 3)), m[(b + 1) >> 2] >> (8 * ((b + 1) & 3)), tab);
+            else if ((uint32_t)b < left)
+                il_step(X, b, m[b >> 2] >> (8 * (b & 3)), tab);
+        }
+        il_normalize(X, left & 7u);
     }
 }
 
@@ -148,18 +217,22 @@ struct Stream {
     }
 };
 
+/* Byte i of a fixed-length stream (any upper bits; compile-time i after unrolling) */
 template <int N>
-__device__ __forceinline__ void lfsr_stream(uint32_t (&P)[8], const Stream<N> &s, const uint4 *__restrict__ tab)
+__device__ __forceinline__ uint32_t stream_byte(const Stream<N> &s, int i)
+{
+    return s.word(i >> 2) >> (8 * (i & 3));
+}
+
+/* the N bytes of s, starting at rotation R0 */
+template <int N, int R0>
+__device__ __forceinline__ void lfsr_stream(uint32_t (&X)[8], const Stream<N> &s, const uint4 *__restrict__ tab)
 {
 #pragma unroll
-    for (int k = 0; k < N / 4; ++k)
-        lfsr_word(P, s.word(k), tab);
-    if (N % 4) {
-        const uint32_t w = s.word(N / 4);
-#pragma unroll
-        for (int b = 0; b < N % 4; ++b)
-            lfsr_step(P, (w >> (8 * b)) & 0xffu, tab);
-    }
+    for (int i = 0; i + 1 < N; i += 2)
+        il_pair(X, R0 + i, stream_byte(s, i), stream_byte(s, i + 1), tab);
+    if (N & 1)
+        il_step(X, R0 + N - 1, stream_byte(s, N - 1), tab);
 }
 
 /* Store the 32-byte register at any alignment without touching neighbours:
@@ -218,22 +291,26 @@ __global__ __launch_bounds__(LFSR_WG) void rs_lfsr_k(const RsDevTables *__restri
     const uint4 *synt = lds + 512 * LFSR_REPL;
 
     for (size_t cw = (size_t)blockIdx.x * LFSR_WG + threadIdx.x; cw < count; cw += (size_t)gridDim.x * LFSR_WG) {
-        uint32_t P[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        uint32_t X[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        uint32_t P[8]; /* remainder bytes in order */
         if (size == FULL_K) { /* uniform: fixed-length streams, all loads in flight up front */
             Stream<FULL_K> sd;
             sd.load(data + cw * dstride);
             if (MODE != MODE_ENCODE) {
                 Stream<RS_NR> sp;
                 sp.load(parity + cw * pstride);
-                lfsr_stream(P, sd, tab);
-                lfsr_stream(P, sp, tab);
+                lfsr_stream<FULL_K, 0>(X, sd, tab);
+                lfsr_stream<RS_NR, FULL_K>(X, sp, tab);
+                il_bytes(P, X, (FULL_K + RS_NR) & 7);
             } else {
-                lfsr_stream(P, sd, tab);
+                lfsr_stream<FULL_K, 0>(X, sd, tab);
+                il_bytes(P, X, FULL_K & 7);
             }
         } else {
-            lfsr_feed(P, data + cw * dstride, size, tab);
+            lfsr_feed(X, data + cw * dstride, size, tab);
             if (MODE != MODE_ENCODE)
-                lfsr_feed(P, parity + cw * pstride, RS_NR, tab);
+                lfsr_feed(X, parity + cw * pstride, RS_NR, tab);
+            il_bytes(P, X, 0);
         }
         if (MODE == MODE_SYNDROME) {
             /* S = sum over remainder bytes m of T_m,lo[r_m & 15] ^ T_m,hi[r_m >> 4] */
@@ -245,14 +322,14 @@ __global__ __launch_bounds__(LFSR_WG) void rs_lfsr_k(const RsDevTables *__restri
                     const uint4 *t0 = synt + (m * 4u) * 16u;
                     const uint4 l0 = t0[rm & 15u], l1 = t0[16u + (rm & 15u)];
                     const uint4 h0 = t0[32u + (rm >> 4)], h1 = t0[48u + (rm >> 4)];
-                    S[0] ^= l0.x ^ h0.x;
-                    S[1] ^= l0.y ^ h0.y;
-                    S[2] ^= l0.z ^ h0.z;
-                    S[3] ^= l0.w ^ h0.w;
-                    S[4] ^= l1.x ^ h1.x;
-                    S[5] ^= l1.y ^ h1.y;
-                    S[6] ^= l1.z ^ h1.z;
-                    S[7] ^= l1.w ^ h1.w;
+                    S[0] = xor3(S[0], l0.x, h0.x);
+                    S[1] = xor3(S[1], l0.y, h0.y);
+                    S[2] = xor3(S[2], l0.z, h0.z);
+                    S[3] = xor3(S[3], l0.w, h0.w);
+                    S[4] = xor3(S[4], l1.x, h1.x);
+                    S[5] = xor3(S[5], l1.y, h1.y);
+                    S[6] = xor3(S[6], l1.z, h1.z);
+                    S[7] = xor3(S[7], l1.w, h1.w);
                 }
             }
             uint4 *o = reinterpret_cast<uint4 *>(out + cw * RS_NR);

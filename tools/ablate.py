@@ -30,7 +30,7 @@ def main():
     ok = torch.zeros(n, dtype=torch.uint8, device=dev)
     cor = torch.zeros(n, dtype=torch.uint8, device=dev)
     s = torch.cuda.current_stream().cuda_stream
-    for stop in (1, 2, 3, 4, 0):
+    for stop in (1, 2, 3, 4, 5, 0):
         os.environ["POPORON_AMD_STOP_AT"] = str(stop)
         rs = P.Poporon.default(device=0)
         cw = cw0.clone()
