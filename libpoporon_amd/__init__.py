@@ -23,7 +23,7 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
-LIB_PATH = os.path.join(HERE, "libpoporon_amd.so")
+LIB_PATH = os.environ.get("POPORON_AMD_LIB") or os.path.join(HERE, "libpoporon_amd.so")  # override: experiments
 INCLUDE_DIR = os.path.join(ROOT, "include")
 
 POPORON_FEC_RS = 1

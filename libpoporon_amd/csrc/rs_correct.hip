@@ -8,12 +8,12 @@
  * integer semantics, so results (bytes, bool, corrected_num) are bit-exact.
  *
  * LDS (163,840 B, all of it):
+ *   lsyn 32 KB   each lane's 32 log-syndromes, [row][lane] (conflict-free).
  *   lgf  64 KB   GF(256) {exp2[x], log[x & 255]} dwords, replicated 32x so
  *                lane l's ds_read_u8 always hits bank l & 31: every random
  *                table lookup is conflict-free.
  *   lch  64 KB   Chien chunk rows: term j (1..16) at 16 consecutive points for
  *                a coefficient of log e (e = 255: zero row), ds_read_b128.
- *   lsyn 32 KB   each lane's 32 log-syndromes, [row][lane] (conflict-free).
  *
  * Control flow is wave-uniform: loops run to the wave's maximum degree (a
  * readfirstlane'd DPP/shuffle max) and every lane's arithmetic inside is
@@ -77,6 +77,23 @@ __device__ __forceinline__ uint32_t zero_bytes16(const uint32_t (&v)[4])
         m |= ((t * 0x10204080u) >> 28) << (4 * d);
     }
     return m;
+}
+
+/* data[0] ^= v (v < 256).  COR_ATOMIC_APPLY (experiment, measured slower:
+ * L2 atomic throughput): a device-scope atomic XOR of the aligned dword that
+ * holds the byte, with no return value, so the wave does not wait for it. */
+#ifndef COR_ATOMIC_APPLY
+#define COR_ATOMIC_APPLY 0
+#endif
+__device__ __forceinline__ void xor_byte(uint8_t *p, uint32_t v)
+{
+#if COR_ATOMIC_APPLY
+    const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+    __hip_atomic_fetch_xor(reinterpret_cast<uint32_t *>(a & ~uintptr_t(3)), v << (8u * (uint32_t)(a & 3u)),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#else
+    *p ^= (uint8_t)v;
+#endif
 }
 
 /* Walks a 256-bit root map over i' = i mod 255 in the reference's order:
@@ -165,8 +182,13 @@ __device__ __forceinline__ bool correct_one(const Gf &gf, const uint4 *__restric
             if ((uint32_t)g <= ub) {
 #pragma unroll
                 for (int i = g; i < g + 8; ++i) {
+                    /* i >= r happens only inside the last group, where
+                     * lam[i] == 0 for every active lane: the read (a row past
+                     * this lane's 32, still inside the LDS block) is masked
+                     * below, and being unconditional it issues back to back
+                     * with the group's other reads */
                     const uint32_t li = lam[i];
-                    const uint32_t s = ((uint32_t)i < r) ? (uint32_t)sr[i * COR_WG] : A0;
+                    const uint32_t s = (uint32_t)sr[i * COR_WG];
                     const uint32_t t = gf.exp(gf.log(li) + s);
                     disc ^= (li != 0u && s != A0) ? t : 0u;
                 }
@@ -392,9 +414,9 @@ __device__ __forceinline__ bool correct_one(const Gf &gf, const uint4 *__restric
                     const uint32_t p = pos ? (uint32_t)pos[n] /* quirk Q1/Q2: slot by root ordinal */
                                            : (uint32_t)((int32_t)k - pad);
                     if (p < size)
-                        data[p] ^= (uint8_t)mag;
+                        xor_byte(data + p, mag);
                     else if (p < size + RS_NR)
-                        parity[p - size] ^= (uint8_t)mag;
+                        xor_byte(parity + p - size, mag);
                 }
             } else if (nz) {
                 /* re-syndrome contribution mag * alpha^((fcr+q)*prim*(254-k)) */
@@ -444,9 +466,13 @@ __global__ __launch_bounds__(COR_WG) void rs_correct_k(const RsDevTables *__rest
                                                        const uint8_t *__restrict__ cnt, uint8_t *__restrict__ ok,
                                                        uint8_t *__restrict__ corrected)
 {
-    __shared__ uint32_t lgf[512 * GF_REPL];  /* 64 KB */
-    __shared__ uint4 lch[16 * 256];          /* 64 KB */
-    __shared__ uint8_t lsyn[RS_NR * COR_WG]; /* 32 KB */
+    /* one block, carved by hand so that the layout is known: the BM
+     * discrepancy reads up to 31 rows past lsyn (masked terms), which land in
+     * lgf */
+    __shared__ uint4 lds[(RS_NR * COR_WG + 512 * GF_REPL * 4 + 16 * 256 * 16) / 16];
+    uint8_t *lsyn = reinterpret_cast<uint8_t *>(lds);                           /* 32 KB */
+    uint32_t *lgf = reinterpret_cast<uint32_t *>(lds + RS_NR * COR_WG / 16);     /* 64 KB */
+    uint4 *lch = lds + (RS_NR * COR_WG + 512 * GF_REPL * 4) / 16;              /* 64 KB */
     for (uint32_t t = threadIdx.x; t < 512u * GF_REPL; t += COR_WG) {
         const uint32_t x = t / GF_REPL;
         lgf[t] = (uint32_t)T->exp2[x] | ((uint32_t)T->log[x & 255u] << 8);

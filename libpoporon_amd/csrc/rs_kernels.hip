@@ -32,9 +32,22 @@
  */
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 #include "rs_device.h"
 
+/* global-memory views (global_load, not flat_load) */
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(1))) const u32x4 gu32x4;
+typedef __attribute__((address_space(1))) const uint32_t gu32;
+
 #define LFSR_WG 1024
+#ifndef LFSR_PREFETCH
+#define LFSR_PREFETCH 0 /* rolling prefetch of the next codeword's chunks: measured slower (0.127 vs 0.118 ms encode) */
+#endif
+#ifndef LFSR_STAGGER
+#define LFSR_STAGGER 0 /* (experiment) odd waves sleep LFSR_STAGGER x 8128 cycles first */
+#endif
 #define LFSR_REPL 16
 
 /* ------------------------------------------------------------------------ */
@@ -134,7 +147,7 @@ __device__ __forceinline__ void il_bytes(uint32_t (&P)[8], const uint32_t (&X)[8
 __device__ __forceinline__ void lfsr_feed(uint32_t (&X)[8], const uint8_t *p, uint32_t n, const uint4 *__restrict__ tab)
 {
     const uintptr_t a = reinterpret_cast<uintptr_t>(p);
-    const uint32_t *w = reinterpret_cast<const uint32_t *>(a & ~uintptr_t(3));
+    gu32 *w = reinterpret_cast<gu32 *>(a & ~uintptr_t(3));
     const uint32_t sh = static_cast<uint32_t>(a & 3u);
     const uint32_t nd = (sh + n + 3u) >> 2; /* dwords holding message bytes */
     if (n == 0)
@@ -173,37 +186,73 @@ __device__ __forceinline__ void lfsr_feed(uint32_t (&X)[8], const uint8_t *p, ui
     }
 }
 
-/* Fixed-length stream of N message bytes at any alignment: all the 16-byte
- * aligned chunks that hold message bytes are loaded up front (dwordx4, one
- * request per 16 B, everything in flight at once), then message dwords are
- * re-aligned in registers: dword k = bytes [4k, 4k+4) = funnel of stream
- * dwords q = k + sh/4 and q+1 by sh%4 bytes, with the per-lane q offset
- * resolved by a 2-level select (no dynamic register indexing). */
+/* Where the next codeword's bytes of one stream are: its 16-byte aligned
+ * chunks and the offset of the first byte in the first chunk.  With no next
+ * codeword for this lane (valid = false) the chunks are read from `fallback`
+ * (a mapped row) and never used: every load is unconditional, so the loop
+ * stays straight-line and the compiler's wait counts stay exact.  The
+ * pointer is explicitly global: a flat load would also count against
+ * lgkmcnt, and every LDS wait of the LFSR steps would then wait for HBM. */
+
+struct NextSrc {
+    gu32x4 *c16;
+    uint32_t sh;
+    __device__ __forceinline__ NextSrc(const uint8_t *p, bool valid, const uint8_t *fallback)
+    {
+        const uintptr_t a = reinterpret_cast<uintptr_t>(valid ? p : fallback);
+        c16 = reinterpret_cast<gu32x4 *>(a & ~uintptr_t(15));
+        sh = static_cast<uint32_t>(a & 15u);
+    }
+};
+
+/* Fixed-length stream of N message bytes at any alignment, in registers: the
+ * 16-byte aligned chunks that hold message bytes (dwordx4 loads), re-aligned
+ * on use: dword k = bytes [4k, 4k+4) = funnel of stream dwords q = k + sh/4
+ * and q+1 by sh%4 bytes, with the per-lane q offset resolved by a 2-level
+ * select (no dynamic register indexing).
+ *
+ * Rolling prefetch: lfsr_stream() reloads the chunks with the NEXT
+ * codeword's chunks as soon as the message dwords that read them have been
+ * consumed, so the next codeword's loads are in flight during this
+ * codeword's LFSR steps (no extra registers; without it every lane's loads
+ * and LFSR steps alternate and HBM idles during the compute). */
 template <int N>
 struct Stream {
     static constexpr int NCH = (N + 30) / 16; /* chunks covering up to 15 + N bytes */
     uint32_t D[NCH * 4 + 4];
     uint32_t sdw, sb;
-    __device__ __forceinline__ void load(const uint8_t *p)
+    __device__ __forceinline__ void chunk(int c, const NextSrc &n)
     {
-        const uintptr_t a = reinterpret_cast<uintptr_t>(p);
-        const uint4 *c16 = reinterpret_cast<const uint4 *>(a & ~uintptr_t(15));
-        const uint32_t sh = static_cast<uint32_t>(a & 15u);
-        sdw = sh >> 2;
-        sb = sh & 3u;
+        /* a chunk past the message may lie on an unmapped page: read chunk 0
+         * instead (its bytes are never fed) */
+        const u32x4 v = n.c16[(uint32_t)(16 * c) < n.sh + (uint32_t)N ? c : 0];
+        D[4 * c] = v.x;
+        D[4 * c + 1] = v.y;
+        D[4 * c + 2] = v.z;
+        D[4 * c + 3] = v.w;
+    }
+    /* second refill batch of lfsr_stream: chunks [NCH/2, NCH), then switch */
+    __device__ __forceinline__ void refill_tail(const NextSrc &n)
+    {
 #pragma unroll
-        for (int c = 0; c < NCH; ++c) {
-            uint4 v = make_uint4(0, 0, 0, 0);
-            if ((uint32_t)(16 * c) < sh + (uint32_t)N) /* chunk holds a message byte: same page */
-                v = c16[c];
-            D[4 * c] = v.x;
-            D[4 * c + 1] = v.y;
-            D[4 * c + 2] = v.z;
-            D[4 * c + 3] = v.w;
-        }
+        for (int c = NCH / 2; c < NCH; ++c)
+            chunk(c, n);
+        retarget(n);
+    }
+    __device__ __forceinline__ void retarget(const NextSrc &n)
+    {
+        sdw = n.sh >> 2;
+        sb = n.sh & 3u;
+    }
+    __device__ __forceinline__ void load(const NextSrc &n)
+    {
+#pragma unroll
+        for (int c = 0; c < NCH; ++c)
+            chunk(c, n);
 #pragma unroll
         for (int t = 0; t < 4; ++t)
             D[NCH * 4 + t] = 0;
+        retarget(n);
     }
     __device__ __forceinline__ uint32_t at(int q) const /* stream dword q + sdw */
     {
@@ -224,15 +273,46 @@ __device__ __forceinline__ uint32_t stream_byte(const Stream<N> &s, int i)
     return s.word(i >> 2) >> (8 * (i & 3));
 }
 
-/* the N bytes of s, starting at rotation R0 */
-template <int N, int R0>
-__device__ __forceinline__ void lfsr_stream(uint32_t (&X)[8], const Stream<N> &s, const uint4 *__restrict__ tab)
+/* The bytes [I0, I1) of s, starting at rotation R0 + I0; s is refilled with
+ * the stream `next` in two batches of consecutive chunks (each batch's loads
+ * of a row hit the same few cache lines back to back): chunks [0, NCH/2)
+ * here, as soon as the last of them is dead (chunk c is dead once message
+ * dword 4c+3, i.e. byte 16c+15, has been fed), the rest by the caller
+ * (Stream::refill_tail) once the stream is consumed. */
+/* compile-time loop: f(std::integral_constant<int, i>) for i = I, I+S, ... < E
+ * (fully unrolled by construction, so register arrays indexed by i stay in
+ * registers however large the body) */
+template <int I, int E, int S, class F>
+__device__ __forceinline__ void static_for(F &&f)
 {
-#pragma unroll
-    for (int i = 0; i + 1 < N; i += 2)
+    if constexpr (I < E) {
+        f(std::integral_constant<int, I>{});
+        static_for<I + S, E, S>(f);
+    }
+}
+
+template <int N, int R0, int I0 = 0, int I1 = N, bool REFILL = true>
+__device__ __forceinline__ void lfsr_stream(uint32_t (&X)[8], Stream<N> &s, const NextSrc &next,
+                                            const uint4 *__restrict__ tab)
+{
+    static_assert(I0 % 2 == 0 && (I1 % 2 == 0 || I1 == N), "byte ranges split at pairs");
+    constexpr int NA = Stream<N>::NCH / 2;
+    constexpr int IA = 16 * (NA - 1) + 14; /* pair after which chunks [0, NA) are dead */
+    static_for<I0, I1 - 1, 2>([&](auto ic) __attribute__((always_inline)) {
+        constexpr int i = decltype(ic)::value;
         il_pair(X, R0 + i, stream_byte(s, i), stream_byte(s, i + 1), tab);
-    if (N & 1)
-        il_step(X, R0 + N - 1, stream_byte(s, N - 1), tab);
+        if constexpr (REFILL && i == IA) {
+#pragma unroll
+            for (int c = 0; c < NA; ++c)
+                s.chunk(c, next);
+        }
+    });
+    if constexpr (I1 == N) {
+        if constexpr (N & 1)
+            il_step(X, R0 + N - 1, stream_byte(s, N - 1), tab);
+        /* the caller refills the rest (s.refill_tail) after its stores, so
+         * that the next iteration's first wait covers only the first batch */
+    }
 }
 
 /* Store the 32-byte register at any alignment without touching neighbours:
@@ -274,11 +354,51 @@ __device__ __forceinline__ void store32_any(uint8_t *o, const uint32_t (&P)[8])
 #define MODE_CHECK 2
 #define FULL_K 223 /* message length of the full-length RS(255,223) code: fixed-stream path */
 
+#define PATH_GENERIC 0 /* any size, any alignment: dword loads per 16 bytes */
+#define PATH_SPLIT 1   /* size 223: data stream (rolling prefetch) + separate parity stream */
+#define PATH_CONTIG 2  /* size 223, parity right after the data: one 255-byte stream (rolling prefetch) */
+
+/* what the kernel does with the final register (remainder bytes P, in order) */
 template <int MODE>
+__device__ __forceinline__ void lfsr_epilogue(const uint32_t (&P)[8], const uint4 *__restrict__ synt, size_t cw,
+                                              uint8_t *__restrict__ parity, size_t pstride,
+                                              uint8_t *__restrict__ out)
+{
+    if (MODE == MODE_SYNDROME) {
+        /* S = sum over remainder bytes m of T_m,lo[r_m & 15] ^ T_m,hi[r_m >> 4] */
+        uint32_t S[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        if ((P[0] | P[1] | P[2] | P[3] | P[4] | P[5] | P[6] | P[7]) != 0u) {
+#pragma unroll
+            for (uint32_t m = 0; m < RS_NR; ++m) {
+                const uint32_t rm = (P[m >> 2] >> (8u * (m & 3u))) & 0xffu;
+                const uint4 *t0 = synt + (m * 4u) * 16u;
+                const uint4 l0 = t0[rm & 15u], l1 = t0[16u + (rm & 15u)];
+                const uint4 h0 = t0[32u + (rm >> 4)], h1 = t0[48u + (rm >> 4)];
+                S[0] = xor3(S[0], l0.x, h0.x);
+                S[1] = xor3(S[1], l0.y, h0.y);
+                S[2] = xor3(S[2], l0.z, h0.z);
+                S[3] = xor3(S[3], l0.w, h0.w);
+                S[4] = xor3(S[4], l1.x, h1.x);
+                S[5] = xor3(S[5], l1.y, h1.y);
+                S[6] = xor3(S[6], l1.z, h1.z);
+                S[7] = xor3(S[7], l1.w, h1.w);
+            }
+        }
+        uint4 *o = reinterpret_cast<uint4 *>(out + cw * RS_NR);
+        o[0] = make_uint4(S[0], S[1], S[2], S[3]);
+        o[1] = make_uint4(S[4], S[5], S[6], S[7]);
+    } else if (MODE == MODE_CHECK) {
+        out[cw] = (P[0] | P[1] | P[2] | P[3] | P[4] | P[5] | P[6] | P[7]) != 0u;
+    } else {
+        store32_any(parity + cw * pstride, P);
+    }
+}
+
+template <int MODE, int PATH>
 __global__ __launch_bounds__(LFSR_WG) void rs_lfsr_k(const RsDevTables *__restrict__ T,
                                                       const uint8_t *__restrict__ data, size_t dstride,
                                                       uint8_t *__restrict__ parity, size_t pstride, uint32_t size,
-                                                      size_t count, uint8_t *__restrict__ out, int par_aligned)
+                                                      size_t count, uint8_t *__restrict__ out)
 {
     __shared__ uint4 lds[512 * LFSR_REPL + (MODE == MODE_SYNDROME ? 32 * 2 * 2 * 16 : 0)];
     for (uint32_t t = threadIdx.x; t < 512u * LFSR_REPL; t += LFSR_WG)
@@ -290,56 +410,72 @@ __global__ __launch_bounds__(LFSR_WG) void rs_lfsr_k(const RsDevTables *__restri
     const uint4 *tab = lds + (threadIdx.x & (LFSR_REPL - 1));
     const uint4 *synt = lds + 512 * LFSR_REPL;
 
-    for (size_t cw = (size_t)blockIdx.x * LFSR_WG + threadIdx.x; cw < count; cw += (size_t)gridDim.x * LFSR_WG) {
-        uint32_t X[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-        uint32_t P[8]; /* remainder bytes in order */
-        if (size == FULL_K) { /* uniform: fixed-length streams, all loads in flight up front */
-            Stream<FULL_K> sd;
-            sd.load(data + cw * dstride);
-            if (MODE != MODE_ENCODE) {
-                Stream<RS_NR> sp;
-                sp.load(parity + cw * pstride);
-                lfsr_stream<FULL_K, 0>(X, sd, tab);
-                lfsr_stream<RS_NR, FULL_K>(X, sp, tab);
-                il_bytes(P, X, (FULL_K + RS_NR) & 7);
-            } else {
-                lfsr_stream<FULL_K, 0>(X, sd, tab);
-                il_bytes(P, X, FULL_K & 7);
-            }
-        } else {
+    const size_t step = (size_t)gridDim.x * LFSR_WG;
+    const size_t cw0 = (size_t)blockIdx.x * LFSR_WG + threadIdx.x;
+    constexpr bool PF = LFSR_PREFETCH != 0;
+    if (LFSR_STAGGER && ((threadIdx.x >> 6) & 1u)) /* experiment: desynchronise odd waves' load bursts */
+        for (int k = 0; k < LFSR_STAGGER; ++k)
+            __builtin_amdgcn_s_sleep(127);
+    if (PATH == PATH_GENERIC) {
+        for (size_t cw = cw0; cw < count; cw += step) {
+            uint32_t X[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+            uint32_t P[8];
             lfsr_feed(X, data + cw * dstride, size, tab);
             if (MODE != MODE_ENCODE)
                 lfsr_feed(X, parity + cw * pstride, RS_NR, tab);
             il_bytes(P, X, 0);
+            lfsr_epilogue<MODE>(P, synt, cw, parity, pstride, out);
         }
-        if (MODE == MODE_SYNDROME) {
-            /* S = sum over remainder bytes m of T_m,lo[r_m & 15] ^ T_m,hi[r_m >> 4] */
-            uint32_t S[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-            if ((P[0] | P[1] | P[2] | P[3] | P[4] | P[5] | P[6] | P[7]) != 0u) {
-#pragma unroll
-                for (uint32_t m = 0; m < RS_NR; ++m) {
-                    const uint32_t rm = (P[m >> 2] >> (8u * (m & 3u))) & 0xffu;
-                    const uint4 *t0 = synt + (m * 4u) * 16u;
-                    const uint4 l0 = t0[rm & 15u], l1 = t0[16u + (rm & 15u)];
-                    const uint4 h0 = t0[32u + (rm >> 4)], h1 = t0[48u + (rm >> 4)];
-                    S[0] = xor3(S[0], l0.x, h0.x);
-                    S[1] = xor3(S[1], l0.y, h0.y);
-                    S[2] = xor3(S[2], l0.z, h0.z);
-                    S[3] = xor3(S[3], l0.w, h0.w);
-                    S[4] = xor3(S[4], l1.x, h1.x);
-                    S[5] = xor3(S[5], l1.y, h1.y);
-                    S[6] = xor3(S[6], l1.z, h1.z);
-                    S[7] = xor3(S[7], l1.w, h1.w);
-                }
+    } else if (PATH == PATH_CONTIG && MODE != MODE_ENCODE) {
+        /* data || parity as one 255-byte stream */
+        Stream<FULL_K + RS_NR> sc;
+        if constexpr (PF) {
+            sc.load(NextSrc(data + cw0 * dstride, cw0 < count, data));
+            __builtin_amdgcn_s_waitcnt(0); /* nothing pending at the loop head but the loop's own refills */
+        }
+        for (size_t cw = cw0; cw < count; cw += step) {
+            const size_t cn = cw + step;
+            uint32_t X[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+            uint32_t P[8];
+            const NextSrc nx(data + cn * dstride, cn < count, data + cw * dstride);
+            if constexpr (!PF)
+                sc.load(NextSrc(data + cw * dstride, true, nullptr));
+            lfsr_stream<FULL_K + RS_NR, 0, 0, 128, PF>(X, sc, nx, tab); /* two loops: each fully unrolled */
+            lfsr_stream<FULL_K + RS_NR, 0, 128, FULL_K + RS_NR, PF>(X, sc, nx, tab);
+            il_bytes(P, X, (FULL_K + RS_NR) & 7);
+            lfsr_epilogue<MODE>(P, synt, cw, parity, pstride, out);
+            if constexpr (PF)
+                sc.refill_tail(nx);
+        }
+    } else {
+        Stream<FULL_K> sd;
+        if constexpr (PF) {
+            sd.load(NextSrc(data + cw0 * dstride, cw0 < count, data));
+            __builtin_amdgcn_s_waitcnt(0); /* nothing pending at the loop head but the loop's own refills */
+        }
+        for (size_t cw = cw0; cw < count; cw += step) {
+            const size_t cn = cw + step;
+            const NextSrc dn(data + cn * dstride, cn < count, data + cw * dstride);
+            uint32_t X[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+            uint32_t P[8];
+            if constexpr (!PF)
+                sd.load(NextSrc(data + cw * dstride, true, nullptr));
+            if (MODE != MODE_ENCODE) {
+                /* the 32 parity bytes: loaded two thirds into the data (in
+                 * flight for ~70 steps, live only from there on) */
+                lfsr_stream<FULL_K, 0, 0, 150, PF>(X, sd, dn, tab);
+                Stream<RS_NR> sp;
+                sp.load(NextSrc(parity + cw * pstride, true, nullptr));
+                lfsr_stream<FULL_K, 0, 150, FULL_K, PF>(X, sd, dn, tab);
+                lfsr_stream<RS_NR, FULL_K, 0, RS_NR, false>(X, sp, NextSrc(nullptr, false, nullptr), tab);
+                il_bytes(P, X, (FULL_K + RS_NR) & 7);
+            } else {
+                lfsr_stream<FULL_K, 0, 0, FULL_K, PF>(X, sd, dn, tab);
+                il_bytes(P, X, FULL_K & 7);
             }
-            uint4 *o = reinterpret_cast<uint4 *>(out + cw * RS_NR);
-            o[0] = make_uint4(S[0], S[1], S[2], S[3]);
-            o[1] = make_uint4(S[4], S[5], S[6], S[7]);
-        } else if (MODE == MODE_CHECK) {
-            out[cw] = (P[0] | P[1] | P[2] | P[3] | P[4] | P[5] | P[6] | P[7]) != 0u;
-        } else {
-            (void)par_aligned;
-            store32_any(parity + cw * pstride, P);
+            lfsr_epilogue<MODE>(P, synt, cw, parity, pstride, out);
+            if constexpr (PF)
+                sd.refill_tail(dn);
         }
     }
 }
@@ -351,36 +487,43 @@ static int persistent_grid(size_t count, int wg, int num_cu)
     return (int)(need < g ? (need ? need : 1) : g);
 }
 
-extern "C" hipError_t rsk_encode(const RsDevTables *tab, const uint8_t *data, size_t dstride, uint8_t *parity,
-                                 size_t pstride, uint32_t size, size_t count, int num_cu, hipStream_t stream)
+template <int MODE>
+static hipError_t launch_lfsr(const RsDevTables *tab, const uint8_t *data, size_t dstride, const uint8_t *parity,
+                              size_t pstride, uint32_t size, size_t count, uint8_t *out, int num_cu,
+                              hipStream_t stream)
 {
     if (count == 0)
         return hipSuccess;
-    const int aligned = ((reinterpret_cast<uintptr_t>(parity) | pstride) & 3u) == 0;
-    hipLaunchKernelGGL(rs_lfsr_k<MODE_ENCODE>, dim3(persistent_grid(count, LFSR_WG, num_cu)), dim3(LFSR_WG), 0,
-                       stream, tab, data, dstride, parity, pstride, size, count, nullptr, aligned);
+    const dim3 grid(persistent_grid(count, LFSR_WG, num_cu)), block(LFSR_WG);
+    uint8_t *par = const_cast<uint8_t *>(parity);
+    if (size != FULL_K)
+        hipLaunchKernelGGL((rs_lfsr_k<MODE, PATH_GENERIC>), grid, block, 0, stream, tab, data, dstride, par, pstride,
+                           size, count, out);
+    else if (MODE != MODE_ENCODE && parity == data + FULL_K && pstride == dstride)
+        hipLaunchKernelGGL((rs_lfsr_k<MODE, PATH_CONTIG>), grid, block, 0, stream, tab, data, dstride, par, pstride,
+                           size, count, out);
+    else
+        hipLaunchKernelGGL((rs_lfsr_k<MODE, PATH_SPLIT>), grid, block, 0, stream, tab, data, dstride, par, pstride,
+                           size, count, out);
     return hipGetLastError();
+}
+
+extern "C" hipError_t rsk_encode(const RsDevTables *tab, const uint8_t *data, size_t dstride, uint8_t *parity,
+                                 size_t pstride, uint32_t size, size_t count, int num_cu, hipStream_t stream)
+{
+    return launch_lfsr<MODE_ENCODE>(tab, data, dstride, parity, pstride, size, count, nullptr, num_cu, stream);
 }
 
 extern "C" hipError_t rsk_syndrome(const RsDevTables *tab, const uint8_t *data, size_t dstride, const uint8_t *parity,
                                    size_t pstride, uint32_t size, size_t count, uint8_t *syn, int num_cu,
                                    hipStream_t stream)
 {
-    if (count == 0)
-        return hipSuccess;
-    hipLaunchKernelGGL(rs_lfsr_k<MODE_SYNDROME>, dim3(persistent_grid(count, LFSR_WG, num_cu)), dim3(LFSR_WG), 0,
-                       stream, tab, data, dstride, const_cast<uint8_t *>(parity), pstride, size, count, syn, 1);
-    return hipGetLastError();
+    return launch_lfsr<MODE_SYNDROME>(tab, data, dstride, parity, pstride, size, count, syn, num_cu, stream);
 }
 
 extern "C" hipError_t rsk_check(const RsDevTables *tab, const uint8_t *data, size_t dstride, const uint8_t *parity,
                                 size_t pstride, uint32_t size, size_t count, uint8_t *flag, int num_cu,
                                 hipStream_t stream)
 {
-    if (count == 0)
-        return hipSuccess;
-    hipLaunchKernelGGL(rs_lfsr_k<MODE_CHECK>, dim3(persistent_grid(count, LFSR_WG, num_cu)), dim3(LFSR_WG), 0,
-                       stream, tab, data, dstride, const_cast<uint8_t *>(parity), pstride, size, count, flag, 1);
-    return hipGetLastError();
+    return launch_lfsr<MODE_CHECK>(tab, data, dstride, parity, pstride, size, count, flag, num_cu, stream);
 }
-

@@ -1,0 +1,62 @@
+#!/usr/bin/env python3
+"""Time the kernels of one or more library builds (experiments).
+
+    python tools/exp_time.py build/a.so build/b.so ...
+
+Each build runs in its own child process (POPORON_AMD_LIB): 2^20 codewords,
+encode + channel (16 errors) + decode, 3 warm-up + 10 timed round trips;
+prints the average kernel times from the in-library HIP-event timing."""
+import json
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def child():
+    sys.path.insert(0, ROOT)
+    import torch
+    import bench
+    import libpoporon_amd as P
+    n, K, N = 1 << 20, 223, 255
+    dev = torch.device("cuda", 0)
+    rs = P.Poporon.default(device=0)
+    rs.reserve(n)
+    cw = torch.zeros((n, N), dtype=torch.uint8, device=dev)
+    cw[:, :K] = bench.synth_bytes(bench.SEED, 0, n, K, dev)
+    pos, mag = bench.synth_errors(bench.SEED + 1, 0, n, 16, N, dev)
+    pos8, mag8 = pos.to(torch.uint8).contiguous(), mag.to(torch.uint8).contiguous()
+    ok = torch.zeros(n, dtype=torch.uint8, device=dev)
+    cor = torch.zeros(n, dtype=torch.uint8, device=dev)
+    s = torch.cuda.current_stream().cuda_stream
+    b = cw.data_ptr()
+
+    def step():
+        rs.encode_batch_device(b, N, b + K, N, K, n, s)
+        P.channel_xor_device(pos8.data_ptr(), mag8.data_ptr(), 16, b, N, n, s)
+        rs.decode_batch_device(b, N, b + K, N, K, n, ok.data_ptr(), cor.data_ptr(), stream=s)
+    for _ in range(3):
+        step()
+    torch.cuda.synchronize()
+    rs.timing(True)
+    for _ in range(10):
+        step()
+    res = {}
+    for k in (P.KERNEL_ENCODE, P.KERNEL_REMAINDER, P.KERNEL_CORRECT):
+        ms, c = rs.timing_read(k)
+        res[P.KERNEL_NAMES[k]] = round(ms / max(c, 1), 4)
+    res["ok"] = int(ok.sum()) == n and bool((cor == 16).all())
+    print(json.dumps(res))
+
+
+if __name__ == "__main__":
+    if sys.argv[1:] == ["--child"]:
+        child()
+        sys.exit(0)
+    for lib in sys.argv[1:]:
+        env = dict(os.environ, POPORON_AMD_LIB=os.path.abspath(lib))
+        r = subprocess.run([sys.executable, __file__, "--child"], env=env, capture_output=True, text=True,
+                           timeout=300)
+        out = r.stdout.strip().splitlines()
+        print(f"{os.path.basename(lib)}: {out[-1] if out else 'FAILED ' + r.stderr[-300:]}", flush=True)
