@@ -4,23 +4,32 @@
  * rs_correct_k: syndromes in, corrected codewords out; one codeword per lane,
  * 1024-thread persistent workgroups (one per CU).  Follows src/decode.c:17-230
  * of the reference step by step (erasure locator, Berlekamp-Massey in Karn's
- * form, Chien search, Omega, Forney, re-syndrome check, apply), with the same
+ * form, Omega, Chien search, Forney, re-syndrome check, apply), with the same
  * integer semantics, so results (bytes, bool, corrected_num) are bit-exact.
  *
- * LDS (163,840 B, all of it):
- *   lsyn 32 KB   each lane's 32 log-syndromes, [row][lane] (conflict-free).
- *   lgf  64 KB   GF(256) {exp2[x], log[x & 255]} dwords, replicated 32x so
- *                lane l's ds_read_u8 always hits bank l & 31: every random
- *                table lookup is conflict-free.
- *   lch  64 KB   Chien chunk rows: term j (1..16) at 16 consecutive points for
- *                a coefficient of log e (e = 255: zero row), ds_read_b128.
+ * LDS (163,840 B, all of it; the order matters):
+ *   lsyn [0, 32K)     each lane's 32 log-syndromes (byte, 255 = zero),
+ *                     [row][lane]: conflict-free.
+ *   lch  [32K, 96K)   Chien chunk rows: term j (1..16) at 16 consecutive
+ *                     points for a coefficient of log e (e = 255: zero row),
+ *                     ds_read_b128.
+ *   lgf  [96K, 160K)  GF(256) dwords {exp2[x] (byte 0), log16[x & 255]
+ *                     (bytes 2-3)}, x < 512, replicated 32x so that lane l's
+ *                     reads always hit bank l & 31 (conflict-free).
+ *
+ * Zero sentinel.  In registers the log of zero is ZL = 1024 (log16[0] = ZL),
+ * and every valid log is reduced (< 255).  A product is exp(a + b): with
+ * both logs valid a + b <= 508 indexes lgf; with either one a zero the index
+ * is >= 512 and the address lies past the end of the workgroup's LDS
+ * allocation, where gfx950 returns 0 (probed: tools/probes/lds_oob.hip,
+ * profiles/r01_lds_oob_probe.log).  So GF multiply-accumulate needs no zero
+ * tests: one add, one address, one ds_read_u8, one XOR.
  *
  * Control flow is wave-uniform: loops run to the wave's maximum degree (a
- * readfirstlane'd DPP/shuffle max) and every lane's arithmetic inside is
- * branch-free (zero coefficients contribute zero), so the LDS lookups of a
- * group of terms issue back to back instead of serialising behind per-lane
- * branches.  Roots are walked in ascending order by a divergence-free
- * "first set bit of a 256-bit map" iterator.
+ * ballot-based max over the active lanes) in groups of 4 terms; inside a
+ * group every lane's arithmetic is branch-free, so a group's LDS lookups
+ * issue back to back.  Roots are walked in ascending order by a
+ * divergence-free "first set bit of a 256-bit map" iterator.
  *
  * The re-syndrome check (src/decode.c:193-209) is run whenever it can fail:
  * when the locator degree is below the BM length L, or when the reference's
@@ -37,17 +46,42 @@
 #define COR_WG 1024
 #define GF_REPL 32
 #define A0 RS_A0
+#define ZL 1024u         /* log of zero (registers): exp(ZL + anything) reads past the LDS block -> 0 */
+#define BIG 0x10000000u  /* log of zero in the Chien index walk (survives 255 reductions, clamped to 255) */
+
+#define LDS_SYN 0u
+#define LDS_CH (RS_NR * COR_WG)
+#define LDS_GF (LDS_CH + 16u * 256u * 16u)
+#define LDS_END (LDS_GF + 512u * GF_REPL * 4u)
+static_assert(LDS_END == 163840u, "lgf must end exactly at the end of the 160 KiB LDS allocation");
 
 struct Gf {
-    const uint8_t *p; /* table base + (lane & 31) * 4 */
-    __device__ __forceinline__ uint32_t exp(uint32_t x) const { return p[x * (GF_REPL * 4)]; }     /* x < 512 */
-    __device__ __forceinline__ uint32_t log(uint32_t v) const { return p[v * (GF_REPL * 4) + 1]; } /* v < 256 */
+    const uint8_t *p; /* lgf + (lane & 31) * 4 */
+    /* alpha^x for x < 511; 0 for x >= 512 (past the allocation) -- x < 2^24 */
+    __device__ __forceinline__ uint32_t exp(uint32_t x) const { return p[x * (GF_REPL * 4)]; }
+    /* log of v < 256 as a register log: ZL for 0 */
+    __device__ __forceinline__ uint32_t log(uint32_t v) const
+    {
+        return *reinterpret_cast<const uint16_t *>(p + v * (GF_REPL * 4) + 2);
+    }
 };
 
 /* gf_mod of src/internal/common.h:102-110 on the uint16 truncation of v */
 __device__ __forceinline__ uint32_t mod255(uint32_t v) { return (v & 0xffffu) % 255u; }
-/* x < 510 -> x mod 255 */
-__device__ __forceinline__ uint32_t red(uint32_t x) { return x >= 255u ? x - 255u : x; }
+/* x < 510 -> x mod 255; sentinel x >= 767 -> x - 255 (still >= 512) */
+__device__ __forceinline__ uint32_t red(uint32_t x) { return min(x, x - 255u); }
+/* stored byte log (255 = zero) -> register log: max(s, (s - 254) * 1024) as
+ * signed ints is s for s <= 254 and 1024 for 255 (mad + max, no compare) */
+__device__ __forceinline__ uint32_t conv(uint32_t s8)
+{
+    return (uint32_t)max((int32_t)s8, ((int32_t)s8 - 254) * (int32_t)ZL);
+}
+
+/* a ^ b ^ c in one VALU op (gfx950 v_bitop3_b32, truth table 0x96) */
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c)
+{
+    return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+}
 
 /* Maximum of v (< 64) over the ACTIVE lanes of the wave, bit by bit from
  * ballots.  (A shuffle butterfly is wrong here: lanes that have left the
@@ -77,23 +111,6 @@ __device__ __forceinline__ uint32_t zero_bytes16(const uint32_t (&v)[4])
         m |= ((t * 0x10204080u) >> 28) << (4 * d);
     }
     return m;
-}
-
-/* data[0] ^= v (v < 256).  COR_ATOMIC_APPLY (experiment, measured slower:
- * L2 atomic throughput): a device-scope atomic XOR of the aligned dword that
- * holds the byte, with no return value, so the wave does not wait for it. */
-#ifndef COR_ATOMIC_APPLY
-#define COR_ATOMIC_APPLY 0
-#endif
-__device__ __forceinline__ void xor_byte(uint8_t *p, uint32_t v)
-{
-#if COR_ATOMIC_APPLY
-    const uintptr_t a = reinterpret_cast<uintptr_t>(p);
-    __hip_atomic_fetch_xor(reinterpret_cast<uint32_t *>(a & ~uintptr_t(3)), v << (8u * (uint32_t)(a & 3u)),
-                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#else
-    *p ^= (uint8_t)v;
-#endif
 }
 
 /* Walks a 256-bit root map over i' = i mod 255 in the reference's order:
@@ -133,87 +150,97 @@ __device__ __forceinline__ bool correct_one(const Gf &gf, const uint4 *__restric
 {
     const int32_t pad = P.pad;
     const uint32_t size = P.size;
-#define SLOG(k) ((uint32_t)srow[(31u - (k)) * COR_WG]) /* log S_k */
+#define SLOG(k) conv((uint32_t)srow[(31u - (k)) * COR_WG]) /* register log of S_k */
 
-    /* ---- erasure locator prod(1 + X_l x), src/decode.c:31-47 ---- */
+    /* ---- erasure locator prod(1 + X_l x), src/decode.c:31-47 ----
+     * lam[j] ^= X_l * lam[j-1]: terms past the current degree multiply a
+     * zero (log ZL), lanes past their erasure count use X_l = zero. */
     uint32_t lam[RS_NR + 1];
 #pragma unroll
     for (int i = 0; i <= RS_NR; ++i)
         lam[i] = 0;
     lam[0] = 1;
     const uint32_t nemax = wave_max(ne);
-    if (nemax > 0) {
-        if (ne > 0)
-            lam[1] = gf.exp(mod255(P.prim * (uint32_t)(RS_NN - 1u - ((uint32_t)pos[0] + (uint32_t)pad))));
-        for (uint32_t i = 1; i < nemax; ++i) { /* uniform loop; lane active while i < ne */
-            const bool act = i < ne;
-            const uint32_t xl =
-                act ? mod255(P.prim * (uint32_t)(RS_NN - 1u - ((uint32_t)pos[i] + (uint32_t)pad))) : 0u;
+    for (uint32_t i = 0; i < nemax; ++i) { /* uniform */
+        const uint32_t xl = i < ne ? mod255(P.prim * (uint32_t)(RS_NN - 1u - ((uint32_t)pos[i] + (uint32_t)pad))) : ZL;
 #pragma unroll
-            for (int g = RS_NR; g >= 1; g -= 8) {
-                if ((uint32_t)(g - 7) <= i + 1) { /* uniform */
+        for (int g = RS_NR; g >= 1; g -= 4) {
+            if ((uint32_t)(g - 3) <= i + 1) { /* uniform */
 #pragma unroll
-                    for (int j = g; j > g - 8; --j) {
-                        const uint32_t lg = gf.log(lam[j - 1]);
-                        const uint32_t t = gf.exp(xl + lg);
-                        lam[j] ^= (act && (uint32_t)j <= i + 1 && lg != A0) ? t : 0u;
-                    }
-                }
+                for (int j = g; j > g - 4; --j)
+                    lam[j] ^= gf.exp(xl + gf.log(lam[j - 1]));
             }
         }
     }
 
     /* ---- Berlekamp-Massey, src/decode.c:49-96 ----
-     * dl, db: upper bounds of the nonzero indices of lam and of B (log form,
-     * A0 = zero); they only bound the work, exactness comes from the
-     * per-coefficient zero tests. */
-    uint32_t B[RS_NR + 1];
-    uint32_t dl = ne, db = ne, L = ne;
+     * lam: Lambda (poly form) with its logs kept alongside; the logs of
+     * Lambda and of B are packed two per register (u16 halves: entry 2k in
+     * the low half of [k], 2k+1 in the high half; the adds read the halves
+     * through SDWA selects, and B's shift by one entry is one alignbyte per
+     * pair).  dl, db: upper bounds of the nonzero indices of lam and of B;
+     * they only bound the work (zero coefficients contribute zero). */
+#define LLOG(i) (((i) & 1) ? (llp[(i) >> 1] >> 16) : (llp[(i) >> 1] & 0xffffu))
+#define BLOG(i) (((i) & 1) ? (Bp[(i) >> 1] >> 16) : (Bp[(i) >> 1] & 0xffffu))
+    uint32_t llp[RS_NR / 2 + 1], Bp[RS_NR / 2 + 1];
 #pragma unroll
-    for (int i = 0; i <= RS_NR; ++i)
-        B[i] = ((uint32_t)i <= dl) ? gf.log(lam[i]) : A0;
+    for (int k = 0; k <= RS_NR / 2; ++k) {
+        const uint32_t lo = (uint32_t)(2 * k) <= nemax ? gf.log(lam[2 * k]) : ZL;
+        const uint32_t hi = (2 * k + 1 <= RS_NR && (uint32_t)(2 * k + 1) <= nemax) ? gf.log(lam[2 * k + 1]) : ZL;
+        llp[k] = lo | (hi << 16);
+        Bp[k] = llp[k];
+    }
+    uint32_t dl = ne, db = ne, L = ne;
     for (uint32_t r = wave_min(ne) + 1u; r <= RS_NR; ++r) {
         const bool act = r > ne;
         const uint32_t ub = wave_max(act ? dl : 0u); /* <= r - 1 */
         const uint8_t *sr = srow + (RS_NR - r) * COR_WG; /* sr[i*COR_WG] = log S_(r-1-i) */
         uint32_t disc = 0;
 #pragma unroll
-        for (int g = 0; g < RS_NR; g += 8) {
+        for (int g = 0; g < RS_NR; g += 4) {
             if ((uint32_t)g <= ub) {
 #pragma unroll
-                for (int i = g; i < g + 8; ++i) {
+                for (int i = g; i < g + 4; ++i) {
                     /* i >= r happens only inside the last group, where
-                     * lam[i] == 0 for every active lane: the read (a row past
-                     * this lane's 32, still inside the LDS block) is masked
-                     * below, and being unconditional it issues back to back
-                     * with the group's other reads */
-                    const uint32_t li = lam[i];
-                    const uint32_t s = (uint32_t)sr[i * COR_WG];
-                    const uint32_t t = gf.exp(gf.log(li) + s);
-                    disc ^= (li != 0u && s != A0) ? t : 0u;
+                     * lam[i] == 0 for every active lane (log ZL): the row
+                     * read (past this lane's 32, inside the LDS block)
+                     * contributes 0, and being unconditional it issues back
+                     * to back with the group's other reads */
+                    disc ^= gf.exp(LLOG(i) + conv(sr[i * COR_WG]));
                 }
             }
         }
-        disc = gf.log(disc);
-        const bool upd = act && disc != A0;
+        const uint32_t ld = gf.log(disc);
+        const bool upd = act && disc != 0u;
         const bool lengthen = upd && (2u * L <= r + ne - 1u);
         const bool shift = act && !lengthen;
+        const uint32_t dq = upd ? ld : ZL;   /* Lambda += disc * x * B; zero where nothing is updated */
+        const uint32_t nbias = RS_NN - ld;  /* B = Lambda / disc (lengthen only) */
         const uint32_t up = min((uint32_t)RS_NR, max(dl, db + 1u));
         const uint32_t ub2 = wave_max(act ? up : 0u);
+        /* pairs k = 16..0 (entries 2k+1, 2k), top down: pair k reads the old
+         * pair k-1 (B_(2k-1)) before it is rewritten */
 #pragma unroll
-        for (int g = RS_NR; g >= 1; g -= 8) {
-            if ((uint32_t)(g - 7) <= ub2) {
-#pragma unroll
-                for (int i = g; i > g - 8; --i) {
-                    const uint32_t bim1 = B[i - 1], li = lam[i];
-                    const uint32_t t = gf.exp(disc + bim1);
-                    const uint32_t nb = li ? red(gf.log(li) + RS_NN - disc) : A0;
-                    B[i] = lengthen ? nb : (shift ? bim1 : B[i]);
-                    lam[i] = li ^ ((upd && bim1 != A0) ? t : 0u);
+        for (int k = RS_NR / 2; k >= 0; --k) {
+            if ((uint32_t)(2 * k) <= ub2) {
+                const uint32_t blo = k ? BLOG(2 * k - 1) : ZL; /* B_(2k-1): multiplies into lam[2k] */
+                const uint32_t bhi = BLOG(2 * k);              /* B_(2k): into lam[2k+1] */
+                const uint32_t nlo = k ? red(LLOG(2 * k) + nbias) : red(nbias); /* lam[0] == 1 */
+                const uint32_t nhi = red(LLOG(2 * k + 1) + nbias);
+                const uint32_t bsh = k ? __builtin_amdgcn_alignbyte(Bp[k], Bp[k - 1], 2) : ((Bp[0] << 16) | ZL);
+                uint32_t lo = LLOG(2 * k), hi = LLOG(2 * k + 1);
+                if (k) {
+                    lam[2 * k] ^= gf.exp(dq + blo);
+                    lo = gf.log(lam[2 * k]);
                 }
+                if (2 * k + 1 <= RS_NR) {
+                    lam[2 * k + 1] ^= gf.exp(dq + bhi);
+                    hi = gf.log(lam[2 * k + 1]);
+                }
+                Bp[k] = lengthen ? (nlo | (nhi << 16)) : (shift ? bsh : Bp[k]);
+                llp[k] = lo | (hi << 16);
             }
         }
-        B[0] = lengthen ? red(RS_NN - disc) : (shift ? A0 : B[0]); /* lam[0] == 1 */
         if (act) {
             db = lengthen ? dl : min(db + 1u, (uint32_t)RS_NR);
             if (upd)
@@ -222,22 +249,59 @@ __device__ __forceinline__ bool correct_one(const Gf &gf, const uint4 *__restric
                 L = r + ne - L;
         }
     }
+    uint32_t ll[RS_NR + 1];
+#pragma unroll
+    for (int i = 0; i <= RS_NR; ++i)
+        ll[i] = LLOG(i);
+#undef LLOG
+#undef BLOG
 
     if (P.stop_at == 2u)
         return dl > 40u; /* profiling ablation */
 
-    /* ---- log form and degree, src/decode.c:98-110 ---- */
-    uint32_t ll[RS_NR + 1];
+    /* ---- degree, src/decode.c:98-110 ---- */
     uint32_t deg = 0;
 #pragma unroll
-    for (int i = 0; i <= RS_NR; ++i) {
-        ll[i] = ((uint32_t)i <= dl) ? gf.log(lam[i]) : A0;
-        deg = (ll[i] != A0) ? (uint32_t)i : deg;
-    }
+    for (int i = 0; i <= RS_NR; ++i)
+        deg = ll[i] < ZL ? (uint32_t)i : deg;
     if (deg == 0)
         return false;
     const uint32_t degmax = wave_max(deg);
 
+    /* ---- Omega = S * Lambda mod x^deg (log form), src/decode.c:147-158 ----
+     * (computed before the Chien search: it needs only Lambda and S); logs
+     * packed two per register like BM's */
+    uint32_t omp[RS_NR / 2];
+#pragma unroll
+    for (int m = 0; m < RS_NR; ++m) {
+        uint32_t o = ZL;
+        if ((uint32_t)m < degmax) {
+            uint32_t acc = 0;
+#pragma unroll
+            for (int j = 0; j <= m; ++j)
+                acc ^= gf.exp(SLOG((uint32_t)(m - j)) + ll[j]);
+            o = (uint32_t)m < deg ? gf.log(acc) : ZL;
+        }
+        if (m & 1)
+            omp[m >> 1] |= o << 16;
+        else
+            omp[m >> 1] = o;
+    }
+#define OMLOG(m) (((m) & 1) ? (omp[(m) >> 1] >> 16) : (omp[(m) >> 1] & 0xffffu))
+    if (P.stop_at == 3u)
+        return omp[0] > 3000u; /* profiling ablation */
+
+    /* derivative terms (Forney, below): Lambda_(2h+1) for 2h <= min(deg, 31) (src/decode.c:176-180) */
+    const uint32_t dtop = (deg < RS_NR - 1 ? deg : RS_NR - 1) & ~1u;
+    const uint32_t dtopmax = wave_max(dtop);
+    uint32_t loddp[RS_NR / 4]; /* packed like omp: h = 2q (low), 2q+1 (high) */
+#pragma unroll
+    for (int q = 0; q < RS_NR / 4; ++q) {
+        const uint32_t lo = (uint32_t)(4 * q) <= dtop ? ll[4 * q + 1] : ZL;
+        const uint32_t hi = (uint32_t)(4 * q + 2) <= dtop ? ll[4 * q + 3] : ZL;
+        loddp[q] = lo | (hi << 16);
+    }
+#define LODD(h) (((h) & 1) ? (loddp[(h) >> 1] >> 16) : (loddp[(h) >> 1] & 0xffffu))
     /* ---- Chien search: root map over the 255 points ----
      * With num_roots erasures BM does not run (src/decode.c:55) and Lambda is
      * exactly prod(1 + X_l x): its roots are the points alpha^i with
@@ -252,19 +316,28 @@ __device__ __forceinline__ bool correct_one(const Gf &gf, const uint4 *__restric
         uint32_t ej[17];
 #pragma unroll
         for (int j = 1; j <= 16; ++j)
-            ej[j] = ll[j];
+            ej[j] = ll[j] < ZL ? ll[j] : BIG;
 #pragma unroll
         for (int a = 0; a < 16; ++a) {
             uint32_t acc[4] = {0x01010101u, 0x01010101u, 0x01010101u, 0x01010101u};
 #pragma unroll
-            for (int j = 1; j <= 16; ++j) {
+            for (int j = 1; j <= 16; j += 2) {
                 if ((uint32_t)j <= degsearch) {
-                    const uint4 row = chien[(j - 1) * 256 + ej[j]];
-                    acc[0] ^= row.x;
-                    acc[1] ^= row.y;
-                    acc[2] ^= row.z;
-                    acc[3] ^= row.w;
-                    ej[j] = (ej[j] == A0) ? A0 : red(ej[j] + (16u * j) % 255u);
+                    const uint4 r1 = chien[(j - 1) * 256 + min(ej[j], A0)];
+                    ej[j] = red(ej[j] + (16u * j) % 255u);
+                    if ((uint32_t)j + 1u <= degsearch) {
+                        const uint4 r2 = chien[j * 256 + min(ej[j + 1], A0)];
+                        ej[j + 1] = red(ej[j + 1] + (16u * (j + 1)) % 255u);
+                        acc[0] = xor3(acc[0], r1.x, r2.x);
+                        acc[1] = xor3(acc[1], r1.y, r2.y);
+                        acc[2] = xor3(acc[2], r1.z, r2.z);
+                        acc[3] = xor3(acc[3], r1.w, r2.w);
+                    } else {
+                        acc[0] ^= r1.x;
+                        acc[1] ^= r1.y;
+                        acc[2] ^= r1.z;
+                        acc[3] ^= r1.w;
+                    }
                 }
             }
             const uint32_t m16 = zero_bytes16(acc);
@@ -279,7 +352,7 @@ __device__ __forceinline__ bool correct_one(const Gf &gf, const uint4 *__restric
         uint32_t reg[RS_NR + 1];
 #pragma unroll
         for (int j = 1; j <= RS_NR; ++j)
-            reg[j] = ll[j];
+            reg[j] = ll[j] < ZL ? ll[j] : BIG;
 #pragma unroll
         for (int w = 0; w < 8; ++w) {
             uint32_t bits = 0;
@@ -289,10 +362,8 @@ __device__ __forceinline__ bool correct_one(const Gf &gf, const uint4 *__restric
                 uint32_t acc = 1;
 #pragma unroll
                 for (int j = 1; j <= RS_NR; ++j) {
-                    const uint32_t rj = red(reg[j] + j);
-                    const bool nz = reg[j] != A0;
-                    reg[j] = nz ? rj : A0;
-                    acc ^= nz ? gf.exp(rj) : 0u;
+                    reg[j] = red(reg[j] + j);
+                    acc ^= gf.exp(min(reg[j], 511u)); /* exp2[511] = 0 */
                 }
                 bits |= (acc == 0 ? 1u : 0u) << b;
             }
@@ -301,7 +372,7 @@ __device__ __forceinline__ bool correct_one(const Gf &gf, const uint4 *__restric
         uint32_t acc = 1; /* point i = 255 (alpha^0) */
 #pragma unroll
         for (int j = 1; j <= RS_NR; ++j)
-            acc ^= (reg[j] != A0) ? gf.exp(red(reg[j] + j)) : 0u;
+            acc ^= gf.exp(min(red(reg[j] + j), 511u));
         rb[0] |= (acc == 0 ? 1u : 0u);
     }
     if (wave_max(direct ? 1u : 0u)) {
@@ -325,7 +396,7 @@ __device__ __forceinline__ bool correct_one(const Gf &gf, const uint4 *__restric
         cnt += __popc(rb[w]);
     if (cnt != deg)
         return false; /* src/decode.c:143-145 */
-    if (P.stop_at == 3u)
+    if (P.stop_at == 4u)
         return false; /* profiling ablation */
 
     /* locations k = (i*iprim - 1) mod 255 below pad fail, src/decode.c:132-134 */
@@ -341,26 +412,7 @@ __device__ __forceinline__ bool correct_one(const Gf &gf, const uint4 *__restric
             return false;
     }
 
-    /* ---- Omega = S * Lambda mod x^deg (log form), src/decode.c:147-158 ---- */
-    uint32_t om[RS_NR];
-#pragma unroll
-    for (int m = 0; m < RS_NR; ++m) {
-        om[m] = A0;
-        if ((uint32_t)m < degmax) {
-            uint32_t acc = 0;
-#pragma unroll
-            for (int j = 0; j <= m; ++j) {
-                const uint32_t s = SLOG((uint32_t)(m - j)), l = ll[j];
-                const uint32_t t = gf.exp(s + l);
-                acc ^= (s != A0 && l != A0) ? t : 0u;
-            }
-            om[m] = ((uint32_t)m < deg) ? gf.log(acc) : A0;
-        }
-    }
-    if (P.stop_at == 4u)
-        return (om[0] ^ om[1]) > 300u; /* profiling ablation */
-    const uint32_t dtop = (deg < RS_NR - 1 ? deg : RS_NR - 1) & ~1u;
-    const uint32_t dtopmax = wave_max(dtop);
+    const uint32_t nir = max(degmax, dtopmax + 1u); /* powers i*m needed: m < nir */
     const uint32_t cntmax = wave_max(cnt);
     /* the check can fail only if deg < L, or where the reference's int16
      * exponent (src/decode.c:201-202) overflows (then it is not the math) */
@@ -381,43 +433,41 @@ __device__ __forceinline__ bool correct_one(const Gf &gf, const uint4 *__restric
         for (uint32_t n = 0; n < cntmax; ++n) {
             const bool act = run && n < cnt;
             const uint32_t i = it.next(); /* root, ascending as in the reference */
-            uint32_t num = 0, ir = 0;
+            /* the byte this root corrects, loaded now so that the load's
+             * latency overlaps the Forney sums (stored below if nonzero) */
+            const uint32_t k = (i * P.iprim + 254u) % 255u;
+            const uint32_t p = pos ? (uint32_t)pos[n] /* quirk Q1/Q2: slot by root ordinal */
+                                   : (uint32_t)((int32_t)k - pad);
+            uint8_t *tgt = p < size ? data + p : (p < size + RS_NR ? parity + (p - size) : data);
+            const uint32_t old = pass == 1u ? (uint32_t)*tgt : 0u;
+            /* num = sum_m Omega_m a^(i m), den = sum_h Lambda_(2h+1) a^(2h i):
+             * a^(i m) as two interleaved chains of logs (even / odd m) */
+            const uint32_t i1 = i == 255u ? 0u : i;
+            const uint32_t i2 = red(i1 + i1);
+            uint32_t ie = 0, io = i1, num = 0, den = 0;
 #pragma unroll
-            for (int m = 0; m < RS_NR; ++m) {
-                if ((uint32_t)m < degmax) {
-                    const uint32_t t = gf.exp(om[m] + ir);
-                    num ^= (om[m] != A0) ? t : 0u;
-                    ir = red(ir + i);
+            for (int m = 0; m < RS_NR; m += 2) {
+                if ((uint32_t)m < nir) {
+                    if ((uint32_t)m < degmax)
+                        num ^= gf.exp(OMLOG(m) + ie);
+                    if ((uint32_t)m <= dtopmax)
+                        den ^= gf.exp(LODD(m >> 1) + ie);
+                    if ((uint32_t)m + 1u < degmax)
+                        num ^= gf.exp(OMLOG(m + 1) + io);
+                    ie = red(ie + i2);
+                    io = red(io + i2);
                 }
             }
             const uint32_t ln2 = mod255((uint32_t)((int32_t)i * ((int32_t)P.fcr - 1) + (int32_t)RS_NN));
-            const uint32_t i2 = red(i + i);
-            uint32_t den = 0;
-            ir = 0;
-#pragma unroll
-            for (int m = 0; m < RS_NR; m += 2) {
-                if ((uint32_t)m <= dtopmax) {
-                    const uint32_t l = ((uint32_t)m <= dtop) ? ll[m + 1] : A0;
-                    const uint32_t t = gf.exp(l + ir);
-                    den ^= (l != A0) ? t : 0u;
-                    ir = red(ir + i2);
-                }
-            }
-            const uint32_t lmag = (gf.log(num) + ln2 + RS_NN - gf.log(den)) % 255u;
+            const uint32_t lden = min(gf.log(den), A0); /* log 0 = A0 in the reference: no den = 0 guard */
+            const uint32_t lmag = (min(gf.log(num), A0) + ln2 + RS_NN - lden) % 255u;
             const uint32_t mag = gf.exp(lmag);
             const bool nz = act && num != 0u; /* zero numerator: no correction, not counted */
             if (nz && (verify ? pass == 0u : pass == 1u)) /* counted once, before the check */
                 ++corrected;
-            const uint32_t k = (i * P.iprim + 254u) % 255u;
             if (pass == 1u) {
-                if (nz) {
-                    const uint32_t p = pos ? (uint32_t)pos[n] /* quirk Q1/Q2: slot by root ordinal */
-                                           : (uint32_t)((int32_t)k - pad);
-                    if (p < size)
-                        xor_byte(data + p, mag);
-                    else if (p < size + RS_NR)
-                        xor_byte(parity + p - size, mag);
-                }
+                if (nz && p < size + RS_NR)
+                    *tgt = (uint8_t)(old ^ mag);
             } else if (nz) {
                 /* re-syndrome contribution mag * alpha^((fcr+q)*prim*(254-k)) */
                 if (P.vfast) {
@@ -440,10 +490,8 @@ __device__ __forceinline__ bool correct_one(const Gf &gf, const uint4 *__restric
         }
         if (pass == 0u) {
 #pragma unroll
-            for (int q = 0; q < RS_NR; ++q) {
-                const uint32_t s = SLOG((uint32_t)q);
-                V[q >> 2] ^= (s == A0 ? 0u : gf.exp(s)) << (8 * (q & 3));
-            }
+            for (int q = 0; q < RS_NR; ++q)
+                V[q >> 2] ^= gf.exp(SLOG((uint32_t)q)) << (8 * (q & 3)); /* zero S: ZL -> 0 */
             bool same = true;
 #pragma unroll
             for (int q = 0; q < RS_NR / 4; ++q)
@@ -455,6 +503,8 @@ __device__ __forceinline__ bool correct_one(const Gf &gf, const uint4 *__restric
         }
     }
 #undef SLOG
+#undef OMLOG
+#undef LODD
     return good;
 }
 
@@ -466,16 +516,16 @@ __global__ __launch_bounds__(COR_WG) void rs_correct_k(const RsDevTables *__rest
                                                        const uint8_t *__restrict__ cnt, uint8_t *__restrict__ ok,
                                                        uint8_t *__restrict__ corrected)
 {
-    /* one block, carved by hand so that the layout is known: the BM
-     * discrepancy reads up to 31 rows past lsyn (masked terms), which land in
-     * lgf */
-    __shared__ uint4 lds[(RS_NR * COR_WG + 512 * GF_REPL * 4 + 16 * 256 * 16) / 16];
-    uint8_t *lsyn = reinterpret_cast<uint8_t *>(lds);                           /* 32 KB */
-    uint32_t *lgf = reinterpret_cast<uint32_t *>(lds + RS_NR * COR_WG / 16);     /* 64 KB */
-    uint4 *lch = lds + (RS_NR * COR_WG + 512 * GF_REPL * 4) / 16;              /* 64 KB */
+    /* one block, carved by hand: the layout (and lgf ending exactly at the
+     * allocation's end) is part of the arithmetic, see the header */
+    __shared__ uint4 lds[LDS_END / 16];
+    uint8_t *lsyn = reinterpret_cast<uint8_t *>(lds) + LDS_SYN;
+    uint4 *lch = lds + LDS_CH / 16;
+    uint32_t *lgf = reinterpret_cast<uint32_t *>(reinterpret_cast<uint8_t *>(lds) + LDS_GF);
     for (uint32_t t = threadIdx.x; t < 512u * GF_REPL; t += COR_WG) {
         const uint32_t x = t / GF_REPL;
-        lgf[t] = (uint32_t)T->exp2[x] | ((uint32_t)T->log[x & 255u] << 8);
+        const uint32_t v = x & 255u;
+        lgf[t] = (uint32_t)T->exp2[x] | ((v ? (uint32_t)T->log[v] : ZL) << 16);
     }
     for (uint32_t t = threadIdx.x; t < 16u * 256u; t += COR_WG)
         lch[t] = T->chien[t];
@@ -491,7 +541,7 @@ __global__ __launch_bounds__(COR_WG) void rs_correct_k(const RsDevTables *__rest
 #pragma unroll
         for (uint32_t q = 0; q < RS_NR; ++q) {
             const uint32_t v = (sw[q >> 2] >> (8u * (q & 3u))) & 0xffu;
-            const uint32_t lv = syn_is_log ? v : gf.log(v);
+            const uint32_t lv = syn_is_log ? v : min(gf.log(v), A0);
             any |= lv != A0;
             srow[(31u - q) * COR_WG] = (uint8_t)lv;
         }

@@ -39,6 +39,18 @@ for step in "$@"; do
                 python3 tools/kernel_driver.py --reps 3
             i=$((i+1))
         done ;;
+    pmcstages)
+        # correction-kernel counters per ablation stage (tools/ablate_pmc.py, tools/pmc_stages.py)
+        i=0
+        for grp in "SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_BRANCH SQ_WAVE_CYCLES" \
+                   "SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT" \
+                   "SQ_INSTS_SMEM SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAIT_INST_LDS SQ_LDS_IDX_ACTIVE"; do
+            run pmcst$i 300 rocprofv3 --pmc $grp -d gpurun_out/pmcst$i -o pmc --output-format csv -- \
+                python3 tools/ablate_pmc.py
+            i=$((i+1))
+        done
+        python3 tools/pmc_stages.py gpurun_out/pmcst0 gpurun_out/pmcst1 gpurun_out/pmcst2 > gpurun_out/pmc_stages.txt 2>&1
+        cat gpurun_out/pmc_stages.txt ;;
     *) echo "unknown step $step"; exit 2 ;;
     esac
 done
