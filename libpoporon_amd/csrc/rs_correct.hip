@@ -312,39 +312,46 @@ __device__ __forceinline__ bool correct_one(const Gf &gf, const uint4 *__restric
     const uint32_t degsearch = wave_max(direct ? 0u : deg);
     uint32_t rb[8];
     if (degsearch <= 16) {
-        /* chunk a: points i' = 16a + b: Lambda = 1 + sum_j T_j[e_j], e_j = log(Lambda_j) + 16aj */
+        /* chunk a: points i' = 16a + b: Lambda = 1 + sum_j T_j[e_j], e_j = log(Lambda_j) + 16aj.
+         * A rolled loop over chunk pairs (a = 2w, 2w+1): its body stays small
+         * (instruction cache, registers); the 32-bit map words come out in
+         * order and shift through rb. */
         uint32_t ej[17];
 #pragma unroll
         for (int j = 1; j <= 16; ++j)
             ej[j] = ll[j] < ZL ? ll[j] : BIG;
+#pragma unroll 1
+        for (int w = 0; w < 8; ++w) {
+            uint32_t word = 0;
 #pragma unroll
-        for (int a = 0; a < 16; ++a) {
-            uint32_t acc[4] = {0x01010101u, 0x01010101u, 0x01010101u, 0x01010101u};
+            for (int h = 0; h < 2; ++h) {
+                uint32_t acc[4] = {0x01010101u, 0x01010101u, 0x01010101u, 0x01010101u};
 #pragma unroll
-            for (int j = 1; j <= 16; j += 2) {
-                if ((uint32_t)j <= degsearch) {
-                    const uint4 r1 = chien[(j - 1) * 256 + min(ej[j], A0)];
-                    ej[j] = red(ej[j] + (16u * j) % 255u);
-                    if ((uint32_t)j + 1u <= degsearch) {
-                        const uint4 r2 = chien[j * 256 + min(ej[j + 1], A0)];
-                        ej[j + 1] = red(ej[j + 1] + (16u * (j + 1)) % 255u);
-                        acc[0] = xor3(acc[0], r1.x, r2.x);
-                        acc[1] = xor3(acc[1], r1.y, r2.y);
-                        acc[2] = xor3(acc[2], r1.z, r2.z);
-                        acc[3] = xor3(acc[3], r1.w, r2.w);
-                    } else {
-                        acc[0] ^= r1.x;
-                        acc[1] ^= r1.y;
-                        acc[2] ^= r1.z;
-                        acc[3] ^= r1.w;
+                for (int j = 1; j <= 16; j += 2) {
+                    if ((uint32_t)j <= degsearch) {
+                        const uint4 r1 = chien[(j - 1) * 256 + min(ej[j], A0)];
+                        ej[j] = red(ej[j] + (16u * j) % 255u);
+                        if ((uint32_t)j + 1u <= degsearch) {
+                            const uint4 r2 = chien[j * 256 + min(ej[j + 1], A0)];
+                            ej[j + 1] = red(ej[j + 1] + (16u * (j + 1)) % 255u);
+                            acc[0] = xor3(acc[0], r1.x, r2.x);
+                            acc[1] = xor3(acc[1], r1.y, r2.y);
+                            acc[2] = xor3(acc[2], r1.z, r2.z);
+                            acc[3] = xor3(acc[3], r1.w, r2.w);
+                        } else {
+                            acc[0] ^= r1.x;
+                            acc[1] ^= r1.y;
+                            acc[2] ^= r1.z;
+                            acc[3] ^= r1.w;
+                        }
                     }
                 }
+                word |= zero_bytes16(acc) << (16 * h);
             }
-            const uint32_t m16 = zero_bytes16(acc);
-            if (a & 1)
-                rb[a >> 1] |= m16 << 16;
-            else
-                rb[a >> 1] = m16;
+#pragma unroll
+            for (int q = 0; q < 7; ++q)
+                rb[q] = rb[q + 1];
+            rb[7] = word;
         }
         rb[7] &= 0x7FFFFFFFu; /* i' = 255 repeats i' = 0 */
     } else {
