@@ -143,7 +143,7 @@ struct RootIter {
     }
 };
 
-template <typename PosT>
+template <typename PosT, bool ERA>
 __device__ __forceinline__ bool correct_one(const Gf &gf, const uint4 *__restrict__ chien, const uint8_t *srow,
                                             const RsCorrParams &P, uint8_t *data, uint8_t *parity, uint32_t ne,
                                             const PosT *pos, uint32_t &corrected)
@@ -160,7 +160,7 @@ __device__ __forceinline__ bool correct_one(const Gf &gf, const uint4 *__restric
     for (int i = 0; i <= RS_NR; ++i)
         lam[i] = 0;
     lam[0] = 1;
-    const uint32_t nemax = wave_max(ne);
+    const uint32_t nemax = ERA ? wave_max(ne) : 0u; /* error mode: no erasure locator */
     for (uint32_t i = 0; i < nemax; ++i) { /* uniform */
         const uint32_t xl = i < ne ? mod255(P.prim * (uint32_t)(RS_NN - 1u - ((uint32_t)pos[i] + (uint32_t)pad))) : ZL;
 #pragma unroll
@@ -443,7 +443,7 @@ __device__ __forceinline__ bool correct_one(const Gf &gf, const uint4 *__restric
             /* the byte this root corrects, loaded now so that the load's
              * latency overlaps the Forney sums (stored below if nonzero) */
             const uint32_t k = (i * P.iprim + 254u) % 255u;
-            const uint32_t p = pos ? (uint32_t)pos[n] /* quirk Q1/Q2: slot by root ordinal */
+            const uint32_t p = ERA ? (uint32_t)pos[n] /* quirk Q1/Q2: slot by root ordinal */
                                    : (uint32_t)((int32_t)k - pad);
             uint8_t *tgt = p < size ? data + p : (p < size + RS_NR ? parity + (p - size) : data);
             const uint32_t old = pass == 1u ? (uint32_t)*tgt : 0u;
@@ -515,7 +515,7 @@ __device__ __forceinline__ bool correct_one(const Gf &gf, const uint4 *__restric
     return good;
 }
 
-template <typename PosT>
+template <typename PosT, bool ERA>
 __global__ __launch_bounds__(COR_WG) void rs_correct_k(const RsDevTables *__restrict__ T, RsCorrParams P,
                                                        uint8_t *data, size_t dstride, uint8_t *parity, size_t pstride,
                                                        size_t count, const uint8_t *__restrict__ syn, int syn_is_log,
@@ -554,12 +554,12 @@ __global__ __launch_bounds__(COR_WG) void rs_correct_k(const RsDevTables *__rest
         }
         uint32_t fixed = 0;
         bool good = true;
-        const uint32_t ne = pos ? cnt[cw] : 0u;
+        const uint32_t ne = ERA ? cnt[cw] : 0u;
         if (ne > RS_NR)
             good = false; /* undefined behaviour in the reference (quirk Q5): refused */
         else if (any && P.stop_at != 1u)
-            good = correct_one<PosT>(gf, lch, srow, P, data + cw * dstride, parity + cw * pstride, ne,
-                                     pos ? pos + cw * pos_stride : nullptr, fixed);
+            good = correct_one<PosT, ERA>(gf, lch, srow, P, data + cw * dstride, parity + cw * pstride, ne,
+                                          ERA ? pos + cw * pos_stride : nullptr, fixed);
         ok[cw] = good ? 1 : 0;
         if (corrected)
             corrected[cw] = (uint8_t)fixed;
@@ -582,10 +582,13 @@ extern "C" hipError_t rsk_correct(const RsDevTables *tab, const RsCorrParams *pr
         return hipSuccess;
     const dim3 grid(persistent_grid(count, COR_WG, num_cu));
     if (pos32)
-        hipLaunchKernelGGL(rs_correct_k<uint32_t>, grid, dim3(COR_WG), 0, stream, tab, *prm, data, dstride, parity,
-                           pstride, count, syn, syn_is_log, pos32, pos_stride, cnt, ok, corrected);
-    else
-        hipLaunchKernelGGL(rs_correct_k<uint8_t>, grid, dim3(COR_WG), 0, stream, tab, *prm, data, dstride, parity,
-                           pstride, count, syn, syn_is_log, pos8, pos_stride, cnt, ok, corrected);
+        hipLaunchKernelGGL((rs_correct_k<uint32_t, true>), grid, dim3(COR_WG), 0, stream, tab, *prm, data, dstride,
+                           parity, pstride, count, syn, syn_is_log, pos32, pos_stride, cnt, ok, corrected);
+    else if (pos8)
+        hipLaunchKernelGGL((rs_correct_k<uint8_t, true>), grid, dim3(COR_WG), 0, stream, tab, *prm, data, dstride,
+                           parity, pstride, count, syn, syn_is_log, pos8, pos_stride, cnt, ok, corrected);
+    else /* error mode */
+        hipLaunchKernelGGL((rs_correct_k<uint8_t, false>), grid, dim3(COR_WG), 0, stream, tab, *prm, data, dstride,
+                           parity, pstride, count, syn, syn_is_log, pos8, pos_stride, cnt, ok, corrected);
     return hipGetLastError();
 }
