@@ -221,24 +221,30 @@ __device__ __forceinline__ bool correct_one(const Gf &gf, const uint4 *__restric
         /* pairs k = 16..0 (entries 2k+1, 2k), top down: pair k reads the old
          * pair k-1 (B_(2k-1)) before it is rewritten */
 #pragma unroll
-        for (int k = RS_NR / 2; k >= 0; --k) {
-            if ((uint32_t)(2 * k) <= ub2) {
-                const uint32_t blo = k ? BLOG(2 * k - 1) : ZL; /* B_(2k-1): multiplies into lam[2k] */
-                const uint32_t bhi = BLOG(2 * k);              /* B_(2k): into lam[2k+1] */
-                const uint32_t nlo = k ? red(LLOG(2 * k) + nbias) : red(nbias); /* lam[0] == 1 */
-                const uint32_t nhi = red(LLOG(2 * k + 1) + nbias);
-                const uint32_t bsh = k ? __builtin_amdgcn_alignbyte(Bp[k], Bp[k - 1], 2) : ((Bp[0] << 16) | ZL);
-                uint32_t lo = LLOG(2 * k), hi = LLOG(2 * k + 1);
-                if (k) {
-                    lam[2 * k] ^= gf.exp(dq + blo);
-                    lo = gf.log(lam[2 * k]);
+        for (int kmax = RS_NR / 2; kmax >= 0; kmax -= 4) {
+            /* groups of 4 pairs (one basic block each, so that their 8 + 8
+             * lookups issue together); pairs past the bound are harmless:
+             * they see zero logs (ZL) and shift zeros */
+            if ((uint32_t)(2 * max(kmax - 3, 0)) <= ub2) {
+#pragma unroll
+                for (int k = kmax; k > kmax - 4 && k >= 0; --k) {
+                    const uint32_t blo = k ? BLOG(2 * k - 1) : ZL; /* B_(2k-1): multiplies into lam[2k] */
+                    const uint32_t bhi = BLOG(2 * k);              /* B_(2k): into lam[2k+1] */
+                    const uint32_t nlo = k ? red(LLOG(2 * k) + nbias) : red(nbias); /* lam[0] == 1 */
+                    const uint32_t nhi = red(LLOG(2 * k + 1) + nbias);
+                    const uint32_t bsh = k ? __builtin_amdgcn_alignbyte(Bp[k], Bp[k - 1], 2) : ((Bp[0] << 16) | ZL);
+                    uint32_t lo = LLOG(2 * k), hi = LLOG(2 * k + 1);
+                    if (k) {
+                        lam[2 * k] ^= gf.exp(dq + blo);
+                        lo = gf.log(lam[2 * k]);
+                    }
+                    if (2 * k + 1 <= RS_NR) {
+                        lam[2 * k + 1] ^= gf.exp(dq + bhi);
+                        hi = gf.log(lam[2 * k + 1]);
+                    }
+                    Bp[k] = lengthen ? (nlo | (nhi << 16)) : (shift ? bsh : Bp[k]);
+                    llp[k] = lo | (hi << 16);
                 }
-                if (2 * k + 1 <= RS_NR) {
-                    lam[2 * k + 1] ^= gf.exp(dq + bhi);
-                    hi = gf.log(lam[2 * k + 1]);
-                }
-                Bp[k] = lengthen ? (nlo | (nhi << 16)) : (shift ? bsh : Bp[k]);
-                llp[k] = lo | (hi << 16);
             }
         }
         if (act) {
@@ -453,16 +459,18 @@ __device__ __forceinline__ bool correct_one(const Gf &gf, const uint4 *__restric
             const uint32_t i2 = red(i1 + i1);
             uint32_t ie = 0, io = i1, num = 0, den = 0;
 #pragma unroll
-            for (int m = 0; m < RS_NR; m += 2) {
-                if ((uint32_t)m < nir) {
-                    if ((uint32_t)m < degmax)
+            for (int m0 = 0; m0 < RS_NR; m0 += 4) {
+                /* groups of 4 powers (one basic block: 6 lookups together);
+                 * terms past deg / dtop have log ZL and add 0 */
+                if ((uint32_t)m0 < nir) {
+#pragma unroll
+                    for (int m = m0; m < m0 + 4; m += 2) {
                         num ^= gf.exp(OMLOG(m) + ie);
-                    if ((uint32_t)m <= dtopmax)
                         den ^= gf.exp(LODD(m >> 1) + ie);
-                    if ((uint32_t)m + 1u < degmax)
                         num ^= gf.exp(OMLOG(m + 1) + io);
-                    ie = red(ie + i2);
-                    io = red(io + i2);
+                        ie = red(ie + i2);
+                        io = red(io + i2);
+                    }
                 }
             }
             const uint32_t ln2 = mod255((uint32_t)((int32_t)i * ((int32_t)P.fcr - 1) + (int32_t)RS_NN));
