@@ -46,6 +46,12 @@
 #define COR_WG 1024
 #define GF_REPL 32
 #define A0 RS_A0
+#ifndef BM_DISC_G
+#define BM_DISC_G 4 /* BM discrepancy terms per branch-free group */
+#endif
+#ifndef BM_UPD_G
+#define BM_UPD_G 1  /* BM update coefficient pairs per branch-free group (measured: 1 < 2 < 4 < 8) */
+#endif
 #define ZL 1024u         /* log of zero (registers): exp(ZL + anything) reads past the LDS block -> 0 */
 #define BIG 0x10000000u  /* log of zero in the Chien index walk (survives 255 reductions, clamped to 255) */
 
@@ -197,10 +203,10 @@ __device__ __forceinline__ bool correct_one(const Gf &gf, const uint4 *__restric
         const uint8_t *sr = srow + (RS_NR - r) * COR_WG; /* sr[i*COR_WG] = log S_(r-1-i) */
         uint32_t disc = 0;
 #pragma unroll
-        for (int g = 0; g < RS_NR; g += 4) {
+        for (int g = 0; g < RS_NR; g += BM_DISC_G) {
             if ((uint32_t)g <= ub) {
 #pragma unroll
-                for (int i = g; i < g + 4; ++i) {
+                for (int i = g; i < g + BM_DISC_G; ++i) {
                     /* i >= r happens only inside the last group, where
                      * lam[i] == 0 for every active lane (log ZL): the row
                      * read (past this lane's 32, inside the LDS block)
@@ -221,13 +227,13 @@ __device__ __forceinline__ bool correct_one(const Gf &gf, const uint4 *__restric
         /* pairs k = 16..0 (entries 2k+1, 2k), top down: pair k reads the old
          * pair k-1 (B_(2k-1)) before it is rewritten */
 #pragma unroll
-        for (int kmax = RS_NR / 2; kmax >= 0; kmax -= 4) {
+        for (int kmax = RS_NR / 2; kmax >= 0; kmax -= BM_UPD_G) {
             /* groups of 4 pairs (one basic block each, so that their 8 + 8
              * lookups issue together); pairs past the bound are harmless:
              * they see zero logs (ZL) and shift zeros */
-            if ((uint32_t)(2 * max(kmax - 3, 0)) <= ub2) {
+            if ((uint32_t)(2 * max(kmax - (BM_UPD_G - 1), 0)) <= ub2) {
 #pragma unroll
-                for (int k = kmax; k > kmax - 4 && k >= 0; --k) {
+                for (int k = kmax; k > kmax - BM_UPD_G && k >= 0; --k) {
                     const uint32_t blo = k ? BLOG(2 * k - 1) : ZL; /* B_(2k-1): multiplies into lam[2k] */
                     const uint32_t bhi = BLOG(2 * k);              /* B_(2k): into lam[2k+1] */
                     const uint32_t nlo = k ? red(LLOG(2 * k) + nbias) : red(nbias); /* lam[0] == 1 */
@@ -443,18 +449,10 @@ __device__ __forceinline__ bool correct_one(const Gf &gf, const uint4 *__restric
             V[q] = 0;
         RootIter it;
         it.init(rb);
-        for (uint32_t n = 0; n < cntmax; ++n) {
-            const bool act = run && n < cnt;
-            const uint32_t i = it.next(); /* root, ascending as in the reference */
-            /* the byte this root corrects, loaded now so that the load's
-             * latency overlaps the Forney sums (stored below if nonzero) */
-            const uint32_t k = (i * P.iprim + 254u) % 255u;
-            const uint32_t p = ERA ? (uint32_t)pos[n] /* quirk Q1/Q2: slot by root ordinal */
-                                   : (uint32_t)((int32_t)k - pad);
-            uint8_t *tgt = p < size ? data + p : (p < size + RS_NR ? parity + (p - size) : data);
-            const uint32_t old = pass == 1u ? (uint32_t)*tgt : 0u;
-            /* num = sum_m Omega_m a^(i m), den = sum_h Lambda_(2h+1) a^(2h i):
-             * a^(i m) as two interleaved chains of logs (even / odd m) */
+        /* Forney sums of root i: num = sum_m Omega_m a^(i m), den = sum_h
+         * Lambda_(2h+1) a^(2h i), a^(i m) as two interleaved chains of logs
+         * (even / odd m); returns num, sets lmag = log of the magnitude */
+        auto forney = [&](uint32_t i, uint32_t &lmag) __attribute__((always_inline)) {
             const uint32_t i1 = i == 255u ? 0u : i;
             const uint32_t i2 = red(i1 + i1);
             uint32_t ie = 0, io = i1, num = 0, den = 0;
@@ -475,30 +473,69 @@ __device__ __forceinline__ bool correct_one(const Gf &gf, const uint4 *__restric
             }
             const uint32_t ln2 = mod255((uint32_t)((int32_t)i * ((int32_t)P.fcr - 1) + (int32_t)RS_NN));
             const uint32_t lden = min(gf.log(den), A0); /* log 0 = A0 in the reference: no den = 0 guard */
-            const uint32_t lmag = (min(gf.log(num), A0) + ln2 + RS_NN - lden) % 255u;
-            const uint32_t mag = gf.exp(lmag);
-            const bool nz = act && num != 0u; /* zero numerator: no correction, not counted */
-            if (nz && (verify ? pass == 0u : pass == 1u)) /* counted once, before the check */
-                ++corrected;
-            if (pass == 1u) {
-                if (nz && p < size + RS_NR)
-                    *tgt = (uint8_t)(old ^ mag);
-            } else if (nz) {
-                /* re-syndrome contribution mag * alpha^((fcr+q)*prim*(254-k)) */
-                if (P.vfast) {
-                    uint32_t e = (lmag + P.fcr * P.prim * (254u - k)) % 255u;
-                    const uint32_t st = (P.prim * (254u - k)) % 255u;
+            lmag = (min(gf.log(num), A0) + ln2 + RS_NN - lden) % 255u;
+            return num;
+        };
+        auto target = [&](uint32_t p) __attribute__((always_inline)) {
+            return p < size ? data + p : (p < size + RS_NR ? parity + (p - size) : data);
+        };
+        if (!ERA && pass == 1u) {
+            /* error-mode apply, two roots per step: both byte loads are
+             * issued before either root's sums, so their latencies overlap
+             * (the positions of distinct roots are distinct) */
+            for (uint32_t n = 0; n < cntmax; n += 2) {
+                const uint32_t ia = it.next(), ib = it.next(); /* ib = 255 past the last root */
+                const uint32_t pa = (uint32_t)((int32_t)((ia * P.iprim + 254u) % 255u) - pad);
+                const uint32_t pb = (uint32_t)((int32_t)((ib * P.iprim + 254u) % 255u) - pad);
+                uint8_t *ta = target(pa), *tb = target(pb);
+                const uint32_t oa = *ta, ob = *tb;
+                uint32_t la, lb;
+                const uint32_t na = forney(ia, la), nb = forney(ib, lb);
+                const bool za = run && n < cnt && na != 0u, zb = run && n + 1 < cnt && nb != 0u;
+                if (!verify) /* else counted in the check pass */
+                    corrected += (za ? 1u : 0u) + (zb ? 1u : 0u);
+                if (za)
+                    *ta = (uint8_t)(oa ^ gf.exp(la));
+                if (zb)
+                    *tb = (uint8_t)(ob ^ gf.exp(lb));
+            }
+        } else {
+            for (uint32_t n = 0; n < cntmax; ++n) {
+                const bool act = run && n < cnt;
+                const uint32_t i = it.next(); /* root, ascending as in the reference */
+                /* the byte this root corrects, loaded now so that the load's
+                 * latency overlaps the Forney sums (stored below if nonzero) */
+                const uint32_t k = (i * P.iprim + 254u) % 255u;
+                const uint32_t p = ERA ? (uint32_t)pos[n] /* quirk Q1/Q2: slot by root ordinal */
+                                       : (uint32_t)((int32_t)k - pad);
+                uint8_t *tgt = target(p);
+                const uint32_t old = pass == 1u ? (uint32_t)*tgt : 0u;
+                uint32_t lmag;
+                const uint32_t num = forney(i, lmag);
+                const uint32_t mag = gf.exp(lmag);
+                const bool nz = act && num != 0u; /* zero numerator: no correction, not counted */
+                if (nz && (verify ? pass == 0u : pass == 1u)) /* counted once, before the check */
+                    ++corrected;
+                if (pass == 1u) {
+                    if (nz && p < size + RS_NR)
+                        *tgt = (uint8_t)(old ^ mag);
+                } else if (nz) {
+                    /* re-syndrome contribution mag * alpha^((fcr+q)*prim*(254-k)) */
+                    if (P.vfast) {
+                        uint32_t e = (lmag + P.fcr * P.prim * (254u - k)) % 255u;
+                        const uint32_t st = (P.prim * (254u - k)) % 255u;
 #pragma unroll
-                    for (int q = 0; q < RS_NR; ++q) {
-                        V[q >> 2] ^= gf.exp(e) << (8 * (q & 3));
-                        e = red(e + st);
-                    }
-                } else {
+                        for (int q = 0; q < RS_NR; ++q) {
+                            V[q >> 2] ^= gf.exp(e) << (8 * (q & 3));
+                            e = red(e + st);
+                        }
+                    } else {
 #pragma unroll
-                    for (int q = 0; q < RS_NR; ++q) {
-                        const int32_t kk =
-                            (int16_t)((int32_t)(P.fcr + q) * (int32_t)P.prim * (int32_t)(254u - k));
-                        V[q >> 2] ^= gf.exp(mod255((uint32_t)((int32_t)lmag + kk))) << (8 * (q & 3));
+                        for (int q = 0; q < RS_NR; ++q) {
+                            const int32_t kk =
+                                (int16_t)((int32_t)(P.fcr + q) * (int32_t)P.prim * (int32_t)(254u - k));
+                            V[q >> 2] ^= gf.exp(mod255((uint32_t)((int32_t)lmag + kk))) << (8 * (q & 3));
+                        }
                     }
                 }
             }
