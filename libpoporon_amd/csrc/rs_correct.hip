@@ -47,10 +47,13 @@
 #define GF_REPL 32
 #define A0 RS_A0
 #ifndef BM_DISC_G
-#define BM_DISC_G 4 /* BM discrepancy terms per branch-free group */
+#define BM_DISC_G 8 /* BM discrepancy terms per branch-free group */
 #endif
 #ifndef BM_UPD_G
 #define BM_UPD_G 1  /* BM update coefficient pairs per branch-free group (measured: 1 < 2 < 4 < 8) */
+#endif
+#ifndef FORNEY_R
+#define FORNEY_R 4  /* error-mode Forney/apply: roots per step (their byte loads overlap) */
 #endif
 #define ZL 1024u         /* log of zero (registers): exp(ZL + anything) reads past the LDS block -> 0 */
 #define BIG 0x10000000u  /* log of zero in the Chien index walk (survives 255 reductions, clamped to 255) */
@@ -483,21 +486,26 @@ __device__ __forceinline__ bool correct_one(const Gf &gf, const uint4 *__restric
             /* error-mode apply, two roots per step: both byte loads are
              * issued before either root's sums, so their latencies overlap
              * (the positions of distinct roots are distinct) */
-            for (uint32_t n = 0; n < cntmax; n += 2) {
-                const uint32_t ia = it.next(), ib = it.next(); /* ib = 255 past the last root */
-                const uint32_t pa = (uint32_t)((int32_t)((ia * P.iprim + 254u) % 255u) - pad);
-                const uint32_t pb = (uint32_t)((int32_t)((ib * P.iprim + 254u) % 255u) - pad);
-                uint8_t *ta = target(pa), *tb = target(pb);
-                const uint32_t oa = *ta, ob = *tb;
-                uint32_t la, lb;
-                const uint32_t na = forney(ia, la), nb = forney(ib, lb);
-                const bool za = run && n < cnt && na != 0u, zb = run && n + 1 < cnt && nb != 0u;
-                if (!verify) /* else counted in the check pass */
-                    corrected += (za ? 1u : 0u) + (zb ? 1u : 0u);
-                if (za)
-                    *ta = (uint8_t)(oa ^ gf.exp(la));
-                if (zb)
-                    *tb = (uint8_t)(ob ^ gf.exp(lb));
+            for (uint32_t n = 0; n < cntmax; n += FORNEY_R) {
+                uint32_t ir[FORNEY_R], ov[FORNEY_R], lm[FORNEY_R], nm[FORNEY_R];
+                uint8_t *tg[FORNEY_R];
+#pragma unroll
+                for (int t = 0; t < FORNEY_R; ++t) {
+                    ir[t] = it.next(); /* 255 past the last root */
+                    tg[t] = target((uint32_t)((int32_t)((ir[t] * P.iprim + 254u) % 255u) - pad));
+                    ov[t] = *tg[t];
+                }
+#pragma unroll
+                for (int t = 0; t < FORNEY_R; ++t)
+                    nm[t] = forney(ir[t], lm[t]);
+#pragma unroll
+                for (int t = 0; t < FORNEY_R; ++t) {
+                    const bool z = run && n + t < cnt && nm[t] != 0u;
+                    if (!verify) /* else counted in the check pass */
+                        corrected += z ? 1u : 0u;
+                    if (z)
+                        *tg[t] = (uint8_t)(ov[t] ^ gf.exp(lm[t]));
+                }
             }
         } else {
             for (uint32_t n = 0; n < cntmax; ++n) {
