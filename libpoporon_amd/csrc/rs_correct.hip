@@ -109,6 +109,22 @@ __device__ __forceinline__ uint32_t wave_max(uint32_t v)
 
 __device__ __forceinline__ uint32_t wave_min(uint32_t v) { return 63u - wave_max(63u - v); }
 
+/* Maximum of v over all 64 lanes -- only where every lane of the wave is
+ * active (the BM loop: the kernel enters the correction with the whole wave).
+ * DPP row shifts give each row's inclusive maximum in its lane 15, two row
+ * broadcasts fold the rows into lane 63. */
+__device__ __forceinline__ uint32_t wave_max_full(uint32_t v)
+{
+    uint32_t x = v;
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, true)); /* row_shr:1 */
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, true)); /* row_shr:2 */
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, true)); /* row_shr:4 */
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, true)); /* row_shr:8 */
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xa, 0xf, false)); /* row_bcast:15 */
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false)); /* row_bcast:31 */
+    return __builtin_amdgcn_readlane(x, 63);
+}
+
 /* byte-wise zero test of 16 bytes -> 16-bit mask (bit b: byte b is zero) */
 __device__ __forceinline__ uint32_t zero_bytes16(const uint32_t (&v)[4])
 {
@@ -169,7 +185,7 @@ __device__ __forceinline__ bool correct_one(const Gf &gf, const uint4 *__restric
     for (int i = 0; i <= RS_NR; ++i)
         lam[i] = 0;
     lam[0] = 1;
-    const uint32_t nemax = ERA ? wave_max(ne) : 0u; /* error mode: no erasure locator */
+    const uint32_t nemax = ERA ? wave_max_full(ne) : 0u; /* error mode: no erasure locator */
     for (uint32_t i = 0; i < nemax; ++i) { /* uniform */
         const uint32_t xl = i < ne ? mod255(P.prim * (uint32_t)(RS_NN - 1u - ((uint32_t)pos[i] + (uint32_t)pad))) : ZL;
 #pragma unroll
@@ -200,9 +216,9 @@ __device__ __forceinline__ bool correct_one(const Gf &gf, const uint4 *__restric
         Bp[k] = llp[k];
     }
     uint32_t dl = ne, db = ne, L = ne;
-    for (uint32_t r = wave_min(ne) + 1u; r <= RS_NR; ++r) {
+    for (uint32_t r = (ERA ? 63u - wave_max_full(63u - ne) : 0u) + 1u; r <= RS_NR; ++r) {
         const bool act = r > ne;
-        const uint32_t ub = wave_max(act ? dl : 0u); /* <= r - 1 */
+        const uint32_t ub = wave_max_full(act ? dl : 0u); /* <= r - 1 */
         const uint8_t *sr = srow + (RS_NR - r) * COR_WG; /* sr[i*COR_WG] = log S_(r-1-i) */
         uint32_t disc = 0;
 #pragma unroll
@@ -226,7 +242,7 @@ __device__ __forceinline__ bool correct_one(const Gf &gf, const uint4 *__restric
         const uint32_t dq = upd ? ld : ZL;   /* Lambda += disc * x * B; zero where nothing is updated */
         const uint32_t nbias = RS_NN - ld;  /* B = Lambda / disc (lengthen only) */
         const uint32_t up = min((uint32_t)RS_NR, max(dl, db + 1u));
-        const uint32_t ub2 = wave_max(act ? up : 0u);
+        const uint32_t ub2 = wave_max_full(act ? up : 0u);
         /* pairs k = 16..0 (entries 2k+1, 2k), top down: pair k reads the old
          * pair k-1 (B_(2k-1)) before it is rewritten */
 #pragma unroll
@@ -593,29 +609,44 @@ __global__ __launch_bounds__(COR_WG) void rs_correct_k(const RsDevTables *__rest
     const Gf gf{reinterpret_cast<const uint8_t *>(lgf) + (threadIdx.x & (GF_REPL - 1)) * 4};
     uint8_t *srow = lsyn + threadIdx.x;
 
-    for (size_t cw = (size_t)blockIdx.x * COR_WG + threadIdx.x; cw < count; cw += (size_t)gridDim.x * COR_WG) {
-        const uint4 *s4 = reinterpret_cast<const uint4 *>(syn + cw * RS_NR);
-        const uint4 sa = s4[0], sb = s4[1];
-        const uint32_t sw[8] = {sa.x, sa.y, sa.z, sa.w, sb.x, sb.y, sb.z, sb.w};
+    /* The trip count is uniform per workgroup and the whole wave enters the
+     * correction when any of its codewords needs it (the rest, with zero
+     * syndromes, ride through BM as no-ops and leave at deg = 0): the BM
+     * bounds are then full-wave DPP reductions. */
+    for (size_t base = (size_t)blockIdx.x * COR_WG; base < count; base += (size_t)gridDim.x * COR_WG) {
+        const size_t cw = base + threadIdx.x;
+        const bool valid = cw < count;
+        uint32_t sw[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        if (valid) {
+            const uint4 *s4 = reinterpret_cast<const uint4 *>(syn + cw * RS_NR);
+            const uint4 sa = s4[0], sb = s4[1];
+            sw[0] = sa.x, sw[1] = sa.y, sw[2] = sa.z, sw[3] = sa.w;
+            sw[4] = sb.x, sw[5] = sb.y, sw[6] = sb.z, sw[7] = sb.w;
+        }
+        const uint32_t ne0 = (ERA && valid) ? cnt[cw] : 0u;
+        const bool refuse = ne0 > RS_NR; /* undefined behaviour in the reference (quirk Q5): refused */
         bool any = false;
 #pragma unroll
         for (uint32_t q = 0; q < RS_NR; ++q) {
             const uint32_t v = (sw[q >> 2] >> (8u * (q & 3u))) & 0xffu;
-            const uint32_t lv = syn_is_log ? v : min(gf.log(v), A0);
+            const uint32_t lv = (valid && !refuse) ? (syn_is_log ? v : min(gf.log(v), A0)) : A0;
             any |= lv != A0;
             srow[(31u - q) * COR_WG] = (uint8_t)lv;
         }
+        const bool need = any && P.stop_at != 1u;
+        const size_t cs = valid ? cw : 0; /* rows of lanes past the batch: a mapped row, never written */
         uint32_t fixed = 0;
-        bool good = true;
-        const uint32_t ne = ERA ? cnt[cw] : 0u;
-        if (ne > RS_NR)
-            good = false; /* undefined behaviour in the reference (quirk Q5): refused */
-        else if (any && P.stop_at != 1u)
-            good = correct_one<PosT, ERA>(gf, lch, srow, P, data + cw * dstride, parity + cw * pstride, ne,
-                                          ERA ? pos + cw * pos_stride : nullptr, fixed);
-        ok[cw] = good ? 1 : 0;
-        if (corrected)
-            corrected[cw] = (uint8_t)fixed;
+        bool good = !refuse;
+        if (__ballot(need) != 0ull) { /* uniform: the whole wave enters */
+            const bool r = correct_one<PosT, ERA>(gf, lch, srow, P, data + cs * dstride, parity + cs * pstride,
+                                                  need ? ne0 : 0u, ERA ? pos + cs * pos_stride : nullptr, fixed);
+            good = need ? r : good;
+        }
+        if (valid) {
+            ok[cw] = good ? 1 : 0;
+            if (corrected)
+                corrected[cw] = (uint8_t)fixed;
+        }
     }
 }
 
