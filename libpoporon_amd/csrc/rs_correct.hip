@@ -86,6 +86,12 @@ __device__ __forceinline__ uint32_t conv(uint32_t s8)
     return (uint32_t)max((int32_t)s8, ((int32_t)s8 - 254) * (int32_t)ZL);
 }
 
+/* u16 halves of packed log pairs: entry 2k low, 2k+1 high */
+__device__ __forceinline__ uint32_t half(const uint32_t *a, int i)
+{
+    return (i & 1) ? (a[i >> 1] >> 16) : (a[i >> 1] & 0xffffu);
+}
+
 /* a ^ b ^ c in one VALU op (gfx950 v_bitop3_b32, truth table 0x96) */
 __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c)
 {
@@ -216,23 +222,30 @@ __device__ __forceinline__ bool correct_one(const Gf &gf, const uint4 *__restric
         Bp[k] = llp[k];
     }
     uint32_t dl = ne, db = ne, L = ne;
-    for (uint32_t r = (ERA ? 63u - wave_max_full(63u - ne) : 0u) + 1u; r <= RS_NR; ++r) {
+    /* syndrome window: W entry i (u16 halves, packed like llp) = register
+     * log of S_(r-1-i), ZL where r-1-i < 0; one entry shifts in per
+     * iteration, so the discrepancy terms read it from registers */
+    uint32_t W[RS_NR / 2];
+#pragma unroll
+    for (int k = 0; k < RS_NR / 2; ++k)
+        W[k] = ZL | (ZL << 16);
+    const uint32_t r0 = (ERA ? 63u - wave_max_full(63u - ne) : 0u) + 1u;
+    for (uint32_t r = 1; r <= RS_NR; ++r) {
+#pragma unroll
+        for (int k = RS_NR / 2 - 1; k > 0; --k)
+            W[k] = __builtin_amdgcn_alignbyte(W[k], W[k - 1], 2);
+        W[0] = (W[0] << 16) | conv((uint32_t)srow[(RS_NR - r) * COR_WG]); /* S_(r-1) */
+        if (r < r0) /* uniform: before the first codeword's BM step (erasure mode) */
+            continue;
         const bool act = r > ne;
         const uint32_t ub = wave_max_full(act ? dl : 0u); /* <= r - 1 */
-        const uint8_t *sr = srow + (RS_NR - r) * COR_WG; /* sr[i*COR_WG] = log S_(r-1-i) */
         uint32_t disc = 0;
 #pragma unroll
         for (int g = 0; g < RS_NR; g += BM_DISC_G) {
             if ((uint32_t)g <= ub) {
 #pragma unroll
-                for (int i = g; i < g + BM_DISC_G; ++i) {
-                    /* i >= r happens only inside the last group, where
-                     * lam[i] == 0 for every active lane (log ZL): the row
-                     * read (past this lane's 32, inside the LDS block)
-                     * contributes 0, and being unconditional it issues back
-                     * to back with the group's other reads */
-                    disc ^= gf.exp(LLOG(i) + conv(sr[i * COR_WG]));
-                }
+                for (int i = g; i < g + BM_DISC_G; ++i)
+                    disc ^= gf.exp(LLOG(i) + half(W, i)); /* i >= r: window ZL */
             }
         }
         const uint32_t ld = gf.log(disc);
