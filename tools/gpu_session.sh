@@ -23,7 +23,7 @@ run() { # name limit cmd...
 for step in "$@"; do
     case $step in
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
-    tests) run tests 900 python -m pytest tests -m gpu -x -q ;;
+    tests) run tests 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread ;;
     tests_all) run tests_all 900 python -m pytest tests -m gpu -q ;;
     bench) run bench 600 python bench.py ;;
     prof) run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- \
