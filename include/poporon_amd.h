@@ -48,9 +48,13 @@ bool poporon_amd_set_device(poporon_t *pprn, int device);
  * codewords, so that later device calls allocate nothing (graph capture). */
 bool poporon_amd_reserve(poporon_t *pprn, size_t max_count);
 
-/* True when the handle's parameters are served by the GPU kernels
- * (symbol_size 8, num_roots 32, generator without zero coefficients,
- * (fcr+num_roots-1)*prim+254 < 65536); false otherwise. */
+/* True when the handle's parameters are served by the GPU kernels: byte
+ * symbols (2 <= symbol_size <= 8) and 1 <= num_roots < 2^symbol_size - 1,
+ * with any field polynomial, fcr and prim that poporon_create accepts.
+ * RS(255,223)-shaped parameters (symbol_size 8, num_roots 32, generator
+ * without zero coefficients, (fcr+31)*prim+254 < 65536) run on the fast
+ * kernels, all others on the general-parameter kernels (same results,
+ * lower throughput).  False otherwise (symbol_size 1 or > 8). */
 bool poporon_amd_supported(const poporon_t *pprn);
 
 /* ---- device-resident batches (asynchronous on `stream`) ------------------ */
@@ -62,7 +66,7 @@ bool poporon_encode_batch_device(poporon_t *pprn, const uint8_t *d_data, size_t 
  * Decode in place.  d_positions == NULL: errors-only decode (the handle's
  * erasure object and external syndromes, if configured, are NOT used by the
  * batch calls).  Otherwise erasure decode: codeword c's erasure list is
- * d_positions[c*positions_stride .. +32] (uint8 positions into data[], slots
+ * d_positions[c*positions_stride .. +num_roots] (uint8 positions into data[], slots
  * past the count are read exactly as the reference reads its erasure object,
  * quirks Q2/Q3), d_counts[c] its count (<= num_roots).
  * d_ok[c] = decode result (1/0); d_corrected[c] = corrected_num (may be NULL).
@@ -71,6 +75,20 @@ bool poporon_decode_batch_device(poporon_t *pprn, uint8_t *d_data, size_t data_s
                                  size_t parity_stride, size_t size, size_t count, const uint8_t *d_positions,
                                  size_t positions_stride, const uint8_t *d_counts, uint8_t *d_ok,
                                  uint8_t *d_corrected, void *stream);
+
+/*
+ * External-syndrome decode (the config's "syndrome" branch, src/decode.c:
+ * 446-464) for a batch: codeword c's num_roots log-form syndromes (value
+ * 2^symbol_size - 1 = zero, the reference's uint16 type) are
+ * d_syndromes[c*syndrome_stride .. +num_roots].  All-zero syndromes leave the
+ * codeword untouched with d_ok[c] = 1; otherwise the correction runs on them.
+ * A value above 2^symbol_size - 1 (an out-of-table index in the reference)
+ * gives d_ok[c] = 0, d_corrected[c] = 0.
+ */
+bool poporon_decode_batch_syndrome_device(poporon_t *pprn, uint8_t *d_data, size_t data_stride, uint8_t *d_parity,
+                                          size_t parity_stride, size_t size, size_t count,
+                                          const uint16_t *d_syndromes, size_t syndrome_stride, uint8_t *d_ok,
+                                          uint8_t *d_corrected, void *stream);
 
 /* Screening without correction: d_dirty[c] = 1 when codeword c has a nonzero
  * syndrome (the reference's calculate_syndrome_u8 flag, src/decode.c:409-414),

@@ -77,6 +77,8 @@ _SIGS = {
     "poporon_encode_batch_device": (C.c_bool, [_vp, _vp, C.c_size_t, _vp, C.c_size_t, C.c_size_t, C.c_size_t, _vp]),
     "poporon_decode_batch_device": (C.c_bool, [_vp, _vp, C.c_size_t, _vp, C.c_size_t, C.c_size_t, C.c_size_t, _vp,
                                                C.c_size_t, _vp, _vp, _vp, _vp]),
+    "poporon_decode_batch_syndrome_device": (C.c_bool, [_vp, _vp, C.c_size_t, _vp, C.c_size_t, C.c_size_t,
+                                                        C.c_size_t, _vp, C.c_size_t, _vp, _vp, _vp]),
     "poporon_check_batch_device": (C.c_bool, [_vp, _vp, C.c_size_t, _vp, C.c_size_t, C.c_size_t, C.c_size_t, _vp,
                                               _vp]),
     "poporon_encode_batch": (C.c_bool, [_vp, _vp, C.c_size_t, _vp, C.c_size_t, C.c_size_t, C.c_size_t]),
@@ -303,6 +305,15 @@ class Poporon:
         self._check(self.lib.poporon_decode_batch_device(self.h, d_data, data_stride, d_parity, parity_stride, size,
                                                          count, d_positions, positions_stride, d_counts, d_ok,
                                                          d_corrected, stream or None), "poporon_decode_batch_device")
+
+    def decode_batch_syndrome_device(self, d_data, data_stride, d_parity, parity_stride, size, count, d_syndromes,
+                                     syndrome_stride, d_ok, d_corrected=None, stream=0):
+        """External-syndrome branch (src/decode.c:446-464) for a batch: d_syndromes holds num_roots
+        u16 log-form syndromes per codeword, syndrome_stride elements apart."""
+        self._check(self.lib.poporon_decode_batch_syndrome_device(self.h, d_data, data_stride, d_parity,
+                                                                  parity_stride, size, count, d_syndromes,
+                                                                  syndrome_stride, d_ok, d_corrected, stream or None),
+                    "poporon_decode_batch_syndrome_device")
 
     def check_batch_device(self, d_data, data_stride, d_parity, parity_stride, size, count, d_dirty, stream=0):
         self._check(self.lib.poporon_check_batch_device(self.h, d_data, data_stride, d_parity, parity_stride, size,

@@ -28,6 +28,7 @@
 #include "poporon.h"
 #include "poporon_amd.h"
 #include "rs_device.h"
+#include "rs_generic.h"
 
 #ifndef POPORON_BUILDTIME
 #define POPORON_BUILDTIME 1
@@ -117,7 +118,8 @@ struct GpuCtx {
     int device = -1;
     int num_cu = 256;
     hipStream_t stream = nullptr;
-    RsDevTables *tab = nullptr; /* device */
+    RsDevTables *tab = nullptr; /* device (fast kernels) */
+    RsGenTables *gtab = nullptr; /* device (general-parameter kernels) */
     uint8_t *rem = nullptr;     /* device workspace: 32 B per codeword */
     size_t rem_cap = 0;
     /* single-codeword / host-batch staging (device) */
@@ -132,9 +134,13 @@ struct _poporon_t {
     poporon_erasure_t *erasure; /* borrowed, read live at every decode */
     uint16_t *ext_syndrome;     /* borrowed, read live at every decode */
     size_t last_corrected;
-    bool supported;
+    bool supported; /* fast || generic */
+    bool fast;      /* served by the RS(255,223) kernels (rs_kernels.hip, rs_correct.hip) */
+    bool generic;   /* served by the general-parameter kernels (rs_generic.hip) */
     RsDevTables host_tab;
     RsCorrParams corr;
+    RsGenTables gen_tab;
+    RsGenParams gen;
     GpuCtx gpu;
 };
 
@@ -451,6 +457,40 @@ static void build_tables(poporon_t *h)
     p.stop_at = sa ? (uint32_t)atoi(sa) : 0u;
 }
 
+/* General-parameter kernels: byte symbols (2 <= m <= 8) and 1 <= num_roots
+ * < 2^m - 1 (at least one message byte); every field polynomial, fcr and
+ * prim that poporon_create accepts. */
+static bool params_generic(const poporon_t *h)
+{
+    const poporon_rs_t *rs = h->rs;
+    const uint32_t m = rs->gf->symbol_size, nn = rs->gf->field_size;
+    return m >= 2 && m <= 8 && rs->num_roots >= 1 && rs->num_roots < nn && rs->primitive_element != 0;
+}
+
+static void build_generic(poporon_t *h)
+{
+    const poporon_rs_t *rs = h->rs;
+    const poporon_gf_t *gf = rs->gf;
+    RsGenTables &t = h->gen_tab;
+    const uint32_t nn = gf->field_size;
+    memset(&t, 0, sizeof(t));
+    for (uint32_t i = 0; i < 256; i++) {
+        t.alog[i] = i <= nn ? (uint8_t)gf->log2exp[i] : 0;
+        t.log[i] = i <= nn ? (uint8_t)gf->exp2log[i] : (uint8_t)nn;
+    }
+    for (uint32_t i = 0; i <= rs->num_roots; i++)
+        t.gen[i] = (uint8_t)rs->generator_polynomial[i];
+    RsGenParams &p = h->gen;
+    memset(&p, 0, sizeof(p));
+    p.m = gf->symbol_size;
+    p.nn = nn;
+    p.magic = (uint32_t)((1ull << 32) / nn) + 1u;
+    p.fcr = rs->first_consecutive_root;
+    p.prim = rs->primitive_element;
+    p.iprim = h->primitive_inverse;
+    p.nroots = rs->num_roots;
+}
+
 static bool params_supported(const poporon_t *h)
 {
     const poporon_rs_t *rs = h->rs;
@@ -504,9 +544,13 @@ EXPORT poporon_t *poporon_create(const poporon_config_t *config)
     h->erasure = config->erasure;
     h->ext_syndrome = config->syndrome;
     h->last_corrected = 0;
-    h->supported = params_supported(h);
-    if (h->supported)
+    h->fast = params_supported(h);
+    h->generic = !h->fast && params_generic(h);
+    h->supported = h->fast || h->generic;
+    if (h->fast)
         build_tables(h);
+    if (h->generic)
+        build_generic(h);
     return h;
 }
 
@@ -526,6 +570,7 @@ static void gpu_release(GpuCtx &g)
     for (auto e : g.event_pool)
         (void)hipEventDestroy(e);
     (void)hipFree(g.tab);
+    (void)hipFree(g.gtab);
     (void)hipFree(g.rem);
     (void)hipFree(g.stage);
     if (g.stream)
@@ -604,8 +649,8 @@ static bool gpu_init(poporon_t *h)
     if (g.ready)
         return true;
     if (!h->supported)
-        return fail("RS parameters not served by the GPU kernels (need symbol_size 8, num_roots 32, a generator "
-                    "without zero coefficients and (fcr+31)*prim+254 < 65536)");
+        return fail("RS parameters not served by the GPU kernels (need 2 <= symbol_size <= 8 and "
+                    "1 <= num_roots < 2^symbol_size - 1)");
     int n = 0;
     hipError_t e = hipGetDeviceCount(&n);
     if (e != hipSuccess || n == 0)
@@ -623,8 +668,13 @@ static bool gpu_init(poporon_t *h)
     HIP_OK(hipGetDeviceProperties(&prop, g.device));
     g.num_cu = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
     HIP_OK(hipStreamCreateWithFlags(&g.stream, hipStreamNonBlocking));
-    HIP_OK(hipMalloc((void **)&g.tab, sizeof(RsDevTables)));
-    HIP_OK(hipMemcpy(g.tab, &h->host_tab, sizeof(RsDevTables), hipMemcpyHostToDevice));
+    if (h->fast) {
+        HIP_OK(hipMalloc((void **)&g.tab, sizeof(RsDevTables)));
+        HIP_OK(hipMemcpy(g.tab, &h->host_tab, sizeof(RsDevTables), hipMemcpyHostToDevice));
+    } else {
+        HIP_OK(hipMalloc((void **)&g.gtab, sizeof(RsGenTables)));
+        HIP_OK(hipMemcpy(g.gtab, &h->gen_tab, sizeof(RsGenTables), hipMemcpyHostToDevice));
+    }
     g.ready = true;
     return true;
 }
@@ -776,15 +826,32 @@ static bool launch_encode(poporon_t *h, const uint8_t *d_data, size_t ds, uint8_
                           size_t count, hipStream_t s)
 {
     KernelTimer t(h->gpu, POPORON_AMD_KERNEL_ENCODE, s);
-    HIP_OK(rsk_encode(h->gpu.tab, d_data, ds, d_par, ps, (uint32_t)size, count, h->gpu.num_cu, s));
+    if (h->fast) {
+        HIP_OK(rsk_encode(h->gpu.tab, d_data, ds, d_par, ps, (uint32_t)size, count, h->gpu.num_cu, s));
+    } else {
+        RsGenParams prm = h->gen;
+        prm.size = (uint32_t)size;
+        HIP_OK(rsg_encode(h->gpu.gtab, &prm, d_data, ds, d_par, ps, count, h->gpu.num_cu, s));
+    }
     t.done();
     return true;
 }
 
 static bool launch_decode(poporon_t *h, uint8_t *d_data, size_t ds, uint8_t *d_par, size_t ps, size_t size,
-                          size_t count, const uint8_t *ext_syn, const uint8_t *pos8, const uint32_t *pos32,
-                          size_t pos_stride, const uint8_t *cnt, uint8_t *ok, uint8_t *corrected, hipStream_t s)
+                          size_t count, const uint16_t *ext_syn, size_t ext_stride, const uint8_t *pos8,
+                          const uint32_t *pos32, size_t pos_stride, const uint8_t *cnt, uint8_t *ok,
+                          uint8_t *corrected, hipStream_t s)
 {
+    if (!h->fast) {
+        RsGenParams prm = h->gen;
+        prm.size = (uint32_t)size;
+        prm.pad = (int32_t)(h->rs->gf->field_size - h->rs->num_roots - size);
+        KernelTimer t(h->gpu, POPORON_AMD_KERNEL_CORRECT, s);
+        HIP_OK(rsg_decode(h->gpu.gtab, &prm, d_data, ds, d_par, ps, count, ext_syn, ext_stride, pos8, pos32,
+                          pos_stride, cnt, ok, corrected, h->gpu.num_cu, s));
+        t.done();
+        return true;
+    }
     RsCorrParams prm = h->corr;
     prm.size = (uint32_t)size;
     prm.pad = (int32_t)(h->rs->gf->field_size - h->rs->num_roots - size);
@@ -796,8 +863,8 @@ static bool launch_decode(poporon_t *h, uint8_t *d_data, size_t ds, uint8_t *d_p
         t.done();
     }
     KernelTimer t(h->gpu, POPORON_AMD_KERNEL_CORRECT, s);
-    HIP_OK(rsk_correct(h->gpu.tab, &prm, d_data, ds, d_par, ps, count, ext_syn ? ext_syn : h->gpu.rem,
-                       ext_syn ? 1 : 0, pos8, pos32, pos_stride, cnt, ok, corrected, h->gpu.num_cu, s));
+    HIP_OK(rsk_correct(h->gpu.tab, &prm, d_data, ds, d_par, ps, count, h->gpu.rem, ext_syn, ext_stride, pos8, pos32,
+                       pos_stride, cnt, ok, corrected, h->gpu.num_cu, s));
     t.done();
     return true;
 }
@@ -815,8 +882,15 @@ EXPORT bool poporon_check_batch_device(poporon_t *h, const uint8_t *d_data, size
     DeviceGuard dg(h->gpu.device);
     hipStream_t s = (hipStream_t)stream;
     KernelTimer t(h->gpu, POPORON_AMD_KERNEL_CHECK, s);
-    HIP_OK(rsk_check(h->gpu.tab, d_data, data_stride, d_parity, parity_stride, (uint32_t)size, count, d_dirty,
-                     h->gpu.num_cu, s));
+    if (h->fast) {
+        HIP_OK(rsk_check(h->gpu.tab, d_data, data_stride, d_parity, parity_stride, (uint32_t)size, count, d_dirty,
+                         h->gpu.num_cu, s));
+    } else {
+        RsGenParams prm = h->gen;
+        prm.size = (uint32_t)size;
+        HIP_OK(rsg_check(h->gpu.gtab, &prm, d_data, data_stride, d_parity, parity_stride, count, d_dirty,
+                         h->gpu.num_cu, s));
+    }
     t.done();
     return true;
 }
@@ -841,15 +915,33 @@ EXPORT bool poporon_decode_batch_device(poporon_t *h, uint8_t *d_data, size_t da
 {
     if (!h || (count && (!d_data || !d_parity || !d_ok)))
         return fail("NULL argument");
-    if (d_positions && (!d_counts || positions_stride < RS_NR))
-        return fail("erasure batch needs counts and positions_stride >= %d", RS_NR);
+    if (d_positions && (!d_counts || positions_stride < h->rs->num_roots))
+        return fail("erasure batch needs counts and positions_stride >= num_roots (%u)", (unsigned)h->rs->num_roots);
     if (!check_decode_size(h, size))
         return fail("decode size %zu outside [1, %u]", size, (unsigned)(h->rs->gf->field_size - h->rs->num_roots));
     if (!gpu_init(h))
         return false;
     DeviceGuard dg(h->gpu.device);
-    return launch_decode(h, d_data, data_stride, d_parity, parity_stride, size, count, nullptr, d_positions, nullptr,
-                         positions_stride, d_counts, d_ok, d_corrected, (hipStream_t)stream);
+    return launch_decode(h, d_data, data_stride, d_parity, parity_stride, size, count, nullptr, 0, d_positions,
+                         nullptr, positions_stride, d_counts, d_ok, d_corrected, (hipStream_t)stream);
+}
+
+EXPORT bool poporon_decode_batch_syndrome_device(poporon_t *h, uint8_t *d_data, size_t data_stride,
+                                                 uint8_t *d_parity, size_t parity_stride, size_t size, size_t count,
+                                                 const uint16_t *d_syndromes, size_t syndrome_stride, uint8_t *d_ok,
+                                                 uint8_t *d_corrected, void *stream)
+{
+    if (!h || (count && (!d_data || !d_parity || !d_ok || !d_syndromes)))
+        return fail("NULL argument");
+    if (syndrome_stride < h->rs->num_roots)
+        return fail("syndrome_stride < num_roots (%u)", (unsigned)h->rs->num_roots);
+    if (!check_decode_size(h, size))
+        return fail("decode size %zu outside [1, %u]", size, (unsigned)(h->rs->gf->field_size - h->rs->num_roots));
+    if (!gpu_init(h))
+        return false;
+    DeviceGuard dg(h->gpu.device);
+    return launch_decode(h, d_data, data_stride, d_parity, parity_stride, size, count, d_syndromes, syndrome_stride,
+                         nullptr, nullptr, 0, nullptr, d_ok, d_corrected, (hipStream_t)stream);
 }
 
 /* ------------------------------------------------------------------------ */
@@ -914,8 +1006,8 @@ EXPORT bool poporon_decode_batch(poporon_t *h, uint8_t *data, size_t data_stride
 {
     if (!h || (count && (!data || !parity || !ok)))
         return fail("NULL argument");
-    if (positions && (!counts || positions_stride < RS_NR))
-        return fail("erasure batch needs counts and positions_stride >= %d", RS_NR);
+    if (positions && (!counts || positions_stride < h->rs->num_roots))
+        return fail("erasure batch needs counts and positions_stride >= num_roots (%u)", (unsigned)h->rs->num_roots);
     if (!check_decode_size(h, size))
         return fail("decode size %zu outside [1, %u]", size, (unsigned)(h->rs->gf->field_size - h->rs->num_roots));
     if (!gpu_init(h))
@@ -924,25 +1016,25 @@ EXPORT bool poporon_decode_batch(poporon_t *h, uint8_t *data, size_t data_stride
     GpuCtx &g = h->gpu;
     const size_t nr = h->rs->num_roots;
     const size_t chunk = std::min(count, kHostChunk);
-    const size_t per = size + nr + 2 + (positions ? RS_NR + 1 : 0);
+    const size_t per = size + nr + 2 + (positions ? nr + 1 : 0);
     if (!ensure_stage(h, chunk * per + 64))
         return false;
-    std::vector<uint8_t> tmp(chunk * (size + nr + RS_NR + 1));
+    std::vector<uint8_t> tmp(chunk * (size + nr));
     for (size_t c0 = 0; c0 < count; c0 += chunk) {
         const size_t n = std::min(chunk, count - c0);
         uint8_t *dd = g.stage, *dp = dd + n * size, *dok = dp + n * nr, *dcor = dok + n, *dpos = dcor + n,
-                *dcnt = dpos + (positions ? n * RS_NR : 0);
+                *dcnt = dpos + (positions ? n * nr : 0);
         gather(tmp.data(), data + c0 * data_stride, data_stride, size, n);
         gather(tmp.data() + n * size, parity + c0 * parity_stride, parity_stride, nr, n);
         HIP_OK(hipMemcpyAsync(dd, tmp.data(), n * (size + nr), hipMemcpyHostToDevice, g.stream));
         if (positions) {
-            std::vector<uint8_t> pt(n * RS_NR);
-            gather(pt.data(), positions + c0 * positions_stride, positions_stride, RS_NR, n);
-            HIP_OK(hipMemcpyAsync(dpos, pt.data(), n * RS_NR, hipMemcpyHostToDevice, g.stream));
+            std::vector<uint8_t> pt(n * nr);
+            gather(pt.data(), positions + c0 * positions_stride, positions_stride, nr, n);
+            HIP_OK(hipMemcpyAsync(dpos, pt.data(), n * nr, hipMemcpyHostToDevice, g.stream));
             HIP_OK(hipMemcpyAsync(dcnt, counts + c0, n, hipMemcpyHostToDevice, g.stream));
             HIP_OK(hipStreamSynchronize(g.stream));
         }
-        if (!launch_decode(h, dd, size, dp, nr, size, n, nullptr, positions ? dpos : nullptr, nullptr, RS_NR,
+        if (!launch_decode(h, dd, size, dp, nr, size, n, nullptr, 0, positions ? dpos : nullptr, nullptr, nr,
                            positions ? dcnt : nullptr, dok, dcor, g.stream))
             return false;
         HIP_OK(hipMemcpyAsync(tmp.data(), dd, n * (size + nr), hipMemcpyDeviceToHost, g.stream));
@@ -1009,44 +1101,42 @@ EXPORT bool poporon_decode(poporon_t *h, uint8_t *data, size_t size, uint8_t *pa
         DeviceGuard dg(h->gpu.device);
         GpuCtx &g = h->gpu;
         const size_t nr = h->rs->num_roots;
-        /* stage layout: [data | parity | ok | cor | pad | syn(32) or slots(32 x u32) | count] */
+        /* stage layout: [data | parity | ok | cor | pad | syndromes (nr x u16) or slots (nr x u32) | count] */
         const size_t off_p = size, off_ok = size + nr, off_cor = off_ok + 1;
         const size_t off_x = (off_cor + 1 + 15) & ~(size_t)15;
-        if (!ensure_stage(h, off_x + RS_NR * 4 + 16))
+        if (!ensure_stage(h, off_x + nr * 4 + 16))
             return false;
-        uint8_t hostbuf[RS_NR * 4 + 16];
-        const uint8_t *ext = nullptr;
+        std::vector<uint8_t> hostbuf(nr * 4 + 16, 0);
+        const uint16_t *ext = nullptr;
         const uint32_t *pos32 = nullptr;
         const uint8_t *cnt = nullptr;
         bool refuse = false;
         HIP_OK(hipMemcpyAsync(g.stage, data, size, hipMemcpyHostToDevice, g.stream));
         HIP_OK(hipMemcpyAsync(g.stage + off_p, parity, nr, hipMemcpyHostToDevice, g.stream));
         if (h->ext_syndrome) {
-            for (size_t i = 0; i < nr; i++) {
-                if (h->ext_syndrome[i] > 255)
-                    refuse = true; /* out-of-table index in the reference */
-                hostbuf[i] = (uint8_t)h->ext_syndrome[i];
-            }
-            HIP_OK(hipMemcpyAsync(g.stage + off_x, hostbuf, nr, hipMemcpyHostToDevice, g.stream));
-            ext = g.stage + off_x;
+            for (size_t i = 0; i < nr; i++)
+                refuse |= h->ext_syndrome[i] > h->rs->gf->field_size; /* out-of-table index in the reference */
+            memcpy(hostbuf.data(), h->ext_syndrome, nr * sizeof(uint16_t));
+            HIP_OK(hipMemcpyAsync(g.stage + off_x, hostbuf.data(), nr * sizeof(uint16_t), hipMemcpyHostToDevice,
+                                  g.stream));
+            ext = (const uint16_t *)(g.stage + off_x);
         } else if (h->erasure) {
             const poporon_erasure_t *e = h->erasure;
-            uint32_t slots[RS_NR];
-            memset(slots, 0, sizeof(slots));
-            memcpy(slots, e->erasure_positions, std::min<size_t>(e->capacity, RS_NR) * sizeof(uint32_t));
-            if (e->erasure_count > RS_NR)
+            /* the reference reads slots by root ordinal (quirks Q2/Q3): copy nr
+             * slots, those past the list's capacity read as 0 */
+            memcpy(hostbuf.data(), e->erasure_positions, std::min<size_t>(e->capacity, nr) * sizeof(uint32_t));
+            if (e->erasure_count > nr)
                 refuse = true; /* quirk Q5: overflows the locator in the reference */
-            memcpy(hostbuf, slots, sizeof(slots));
-            hostbuf[RS_NR * 4] = (uint8_t)std::min<uint32_t>(e->erasure_count, 255u);
-            HIP_OK(hipMemcpyAsync(g.stage + off_x, hostbuf, RS_NR * 4 + 1, hipMemcpyHostToDevice, g.stream));
+            hostbuf[nr * 4] = (uint8_t)std::min<uint32_t>(e->erasure_count, 255u);
+            HIP_OK(hipMemcpyAsync(g.stage + off_x, hostbuf.data(), nr * 4 + 1, hipMemcpyHostToDevice, g.stream));
             pos32 = (const uint32_t *)(g.stage + off_x);
-            cnt = g.stage + off_x + RS_NR * 4;
+            cnt = g.stage + off_x + nr * 4;
         }
         if (refuse) {
             HIP_OK(hipStreamSynchronize(g.stream));
-            fail("erasure count > num_roots or external syndrome > 255: undefined in the reference, refused");
+            fail("erasure count > num_roots or external syndrome > field size: undefined in the reference, refused");
         } else {
-            if (!launch_decode(h, g.stage, size, g.stage + off_p, nr, size, 1, ext, nullptr, pos32, RS_NR, cnt,
+            if (!launch_decode(h, g.stage, size, g.stage + off_p, nr, size, 1, ext, nr, nullptr, pos32, nr, cnt,
                                g.stage + off_ok, g.stage + off_cor, g.stream))
                 return false;
             uint8_t res[2];

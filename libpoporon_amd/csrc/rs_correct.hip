@@ -600,7 +600,8 @@ __device__ __forceinline__ bool correct_one(const Gf &gf, const uint4 *__restric
 template <typename PosT, bool ERA>
 __global__ __launch_bounds__(COR_WG) void rs_correct_k(const RsDevTables *__restrict__ T, RsCorrParams P,
                                                        uint8_t *data, size_t dstride, uint8_t *parity, size_t pstride,
-                                                       size_t count, const uint8_t *__restrict__ syn, int syn_is_log,
+                                                       size_t count, const uint8_t *__restrict__ syn,
+                                                       const uint16_t *__restrict__ syn16, size_t syn16_stride,
                                                        const PosT *__restrict__ pos, size_t pos_stride,
                                                        const uint8_t *__restrict__ cnt, uint8_t *__restrict__ ok,
                                                        uint8_t *__restrict__ corrected)
@@ -630,19 +631,29 @@ __global__ __launch_bounds__(COR_WG) void rs_correct_k(const RsDevTables *__rest
         const size_t cw = base + threadIdx.x;
         const bool valid = cw < count;
         uint32_t sw[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-        if (valid) {
+        bool ext_bad = false; /* external syndrome > 255: out-of-table in the reference, refused */
+        if (valid && syn16) {
+            /* external log-form syndromes (u16, the reference's type) */
+            const uint16_t *e = syn16 + cw * syn16_stride;
+#pragma unroll
+            for (int q = 0; q < RS_NR; ++q) {
+                const uint32_t v = e[q];
+                ext_bad |= v > 255u;
+                sw[q >> 2] |= (v & 0xffu) << (8 * (q & 3));
+            }
+        } else if (valid) {
             const uint4 *s4 = reinterpret_cast<const uint4 *>(syn + cw * RS_NR);
             const uint4 sa = s4[0], sb = s4[1];
             sw[0] = sa.x, sw[1] = sa.y, sw[2] = sa.z, sw[3] = sa.w;
             sw[4] = sb.x, sw[5] = sb.y, sw[6] = sb.z, sw[7] = sb.w;
         }
         const uint32_t ne0 = (ERA && valid) ? cnt[cw] : 0u;
-        const bool refuse = ne0 > RS_NR; /* undefined behaviour in the reference (quirk Q5): refused */
+        const bool refuse = ne0 > RS_NR || ext_bad; /* undefined behaviour in the reference (quirk Q5): refused */
         bool any = false;
 #pragma unroll
         for (uint32_t q = 0; q < RS_NR; ++q) {
             const uint32_t v = (sw[q >> 2] >> (8u * (q & 3u))) & 0xffu;
-            const uint32_t lv = (valid && !refuse) ? (syn_is_log ? v : min(gf.log(v), A0)) : A0;
+            const uint32_t lv = (valid && !refuse) ? (syn16 ? v : min(gf.log(v), A0)) : A0;
             any |= lv != A0;
             srow[(31u - q) * COR_WG] = (uint8_t)lv;
         }
@@ -671,7 +682,8 @@ static int persistent_grid(size_t count, int wg, int num_cu)
 }
 
 extern "C" hipError_t rsk_correct(const RsDevTables *tab, const RsCorrParams *prm, uint8_t *data, size_t dstride,
-                                  uint8_t *parity, size_t pstride, size_t count, const uint8_t *syn, int syn_is_log,
+                                  uint8_t *parity, size_t pstride, size_t count, const uint8_t *syn,
+                                  const uint16_t *syn16, size_t syn16_stride,
                                   const uint8_t *pos8, const uint32_t *pos32, size_t pos_stride, const uint8_t *cnt,
                                   uint8_t *ok, uint8_t *corrected, int num_cu, hipStream_t stream)
 {
@@ -680,12 +692,12 @@ extern "C" hipError_t rsk_correct(const RsDevTables *tab, const RsCorrParams *pr
     const dim3 grid(persistent_grid(count, COR_WG, num_cu));
     if (pos32)
         hipLaunchKernelGGL((rs_correct_k<uint32_t, true>), grid, dim3(COR_WG), 0, stream, tab, *prm, data, dstride,
-                           parity, pstride, count, syn, syn_is_log, pos32, pos_stride, cnt, ok, corrected);
+                           parity, pstride, count, syn, syn16, syn16_stride, pos32, pos_stride, cnt, ok, corrected);
     else if (pos8)
         hipLaunchKernelGGL((rs_correct_k<uint8_t, true>), grid, dim3(COR_WG), 0, stream, tab, *prm, data, dstride,
-                           parity, pstride, count, syn, syn_is_log, pos8, pos_stride, cnt, ok, corrected);
+                           parity, pstride, count, syn, syn16, syn16_stride, pos8, pos_stride, cnt, ok, corrected);
     else /* error mode */
         hipLaunchKernelGGL((rs_correct_k<uint8_t, false>), grid, dim3(COR_WG), 0, stream, tab, *prm, data, dstride,
-                           parity, pstride, count, syn, syn_is_log, pos8, pos_stride, cnt, ok, corrected);
+                           parity, pstride, count, syn, syn16, syn16_stride, pos8, pos_stride, cnt, ok, corrected);
     return hipGetLastError();
 }

@@ -82,13 +82,16 @@ hipError_t rsk_check(const RsDevTables *tab, const uint8_t *data, size_t dstride
                      uint32_t size, size_t count, uint8_t *flag, int num_cu, hipStream_t stream);
 
 /*
- * Correction.  syn: 32 syndromes per codeword, poly form (from rsk_syndrome)
- * or, with syn_is_log, log form (the config's external "syndrome" pointer
- * path).  pos8 / pos32 (at most one non-NULL) select erasure mode with
- * per-codeword slot arrays of pos_stride entries and counts in cnt.
+ * Correction.  syn: 32 syndromes per codeword, poly form (from rsk_syndrome);
+ * or, when syn16 is non-NULL, 32 log-form u16 syndromes per codeword
+ * syn16_stride elements apart (the config's external "syndrome" branch;
+ * values > 255 refuse the codeword).  pos8 / pos32 (at most one non-NULL)
+ * select erasure mode with per-codeword slot arrays of pos_stride entries
+ * and counts in cnt.
  */
 hipError_t rsk_correct(const RsDevTables *tab, const RsCorrParams *prm, uint8_t *data, size_t dstride, uint8_t *parity,
-                       size_t pstride, size_t count, const uint8_t *syn, int syn_is_log, const uint8_t *pos8,
+                       size_t pstride, size_t count, const uint8_t *syn, const uint16_t *syn16, size_t syn16_stride,
+                       const uint8_t *pos8,
                        const uint32_t *pos32, size_t pos_stride, const uint8_t *cnt, uint8_t *ok, uint8_t *corrected,
                        int num_cu, hipStream_t stream);
 

@@ -1,0 +1,52 @@
+/*
+ * rs_generic.h -- tables, parameters and launchers of the general-parameter
+ * RS kernels (rs_generic.hip): symbol_size 2..8, any num_roots < 2^m - 1.
+ */
+#ifndef POPORON_AMD_RS_GENERIC_H
+#define POPORON_AMD_RS_GENERIC_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#include <hip/hip_runtime.h>
+
+/* device-resident per-handle tables, built by api.cpp from the handle's GF
+ * tables (src/gf.c:29-86) and generator (src/rs.c:29-82) */
+struct RsGenTables {
+    uint8_t alog[256]; /* log2exp: alpha^i for i < nn, alog[nn] = 0 (entries past nn: 0) */
+    uint8_t log[256];  /* exp2log: log[0] = nn (entries past nn: nn) */
+    uint8_t gen[256];  /* generator, log form, gen[0..nroots] */
+};
+
+struct RsGenParams {
+    uint32_t m, nn, magic; /* nn = 2^m - 1; magic = floor(2^32 / nn) + 1 */
+    uint32_t fcr, prim, iprim, nroots;
+    uint32_t size; /* message bytes per codeword */
+    int32_t pad;   /* nn - nroots - size (decode) */
+};
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+hipError_t rsg_encode(const RsGenTables *tab, const RsGenParams *prm, const uint8_t *data, size_t dstride,
+                      uint8_t *parity, size_t pstride, size_t count, int num_cu, hipStream_t stream);
+
+/* ext (nroots u16 log-form syndromes per codeword, ext_stride elements apart)
+ * selects the external-syndrome branch; else pos8/pos32 (at most one non-NULL,
+ * pos_stride entries per codeword, counts in cnt) the erasure branch; else
+ * errors-only decode. */
+hipError_t rsg_decode(const RsGenTables *tab, const RsGenParams *prm, uint8_t *data, size_t dstride, uint8_t *parity,
+                      size_t pstride, size_t count, const uint16_t *ext, size_t ext_stride, const uint8_t *pos8,
+                      const uint32_t *pos32, size_t pos_stride, const uint8_t *cnt, uint8_t *ok, uint8_t *corrected,
+                      int num_cu, hipStream_t stream);
+
+hipError_t rsg_check(const RsGenTables *tab, const RsGenParams *prm, const uint8_t *data, size_t dstride,
+                     const uint8_t *parity, size_t pstride, size_t count, uint8_t *dirty, int num_cu,
+                     hipStream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif

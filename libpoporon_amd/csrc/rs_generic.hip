@@ -1,0 +1,468 @@
+/*
+ * rs_generic.hip -- RS over GF(2^m), any parameters with m <= 8 (gfx950).
+ *
+ * The fast kernels (rs_kernels.hip, rs_correct.hip) are specialised for
+ * symbol_size 8 and num_roots 32.  Every other parameter set that the
+ * reference accepts and that fits byte symbols (2 <= m <= 8, any primitive
+ * field polynomial, any fcr, any prim with a primitive inverse, 1 <= num_roots
+ * < 2^m - 1) is served here, with the reference's integer semantics step by
+ * step:
+ *   rsg_encode_k   systematic LFSR                      src/encode.c:120-143
+ *   rsg_decode_k   syndromes (Horner per root)          src/decode.c:375-415
+ *                  erasure locator, BM, Chien, Omega,
+ *                  Forney, re-syndrome check, apply     src/decode.c:17-230
+ *                  branch logic (ext. syndrome/erasure) src/decode.c:431-487
+ *   rsg_check_k    "any syndrome nonzero" only
+ *
+ * One codeword per lane.  Every per-codeword array (syndromes, locator, B,
+ * Omega, roots, locations, magnitudes; num_roots + 1 bytes each) lives in
+ * LDS laid out [index][lane], so lanes of a wave touch consecutive bytes.
+ * With m <= 8 every field element and every log (A0 = 2^m - 1 is the log of
+ * zero) fits a byte.  The GF tables (log, antilog, generator) are 768 bytes
+ * of LDS shared by the workgroup.
+ *
+ * gf_mod (src/internal/common.h:102-110) takes a uint16 and, for m <= 8,
+ * equals (v mod 2^16) mod (2^m - 1) for every argument (checked exhaustively
+ * in tests/test_library_cpu.py); the kernels compute it with a reciprocal
+ * multiply (exact for arguments < 2^16).
+ */
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+
+#include "rs_generic.h"
+
+#define G_WG_MAX 256
+
+struct GMod {
+    uint32_t nn, magic; /* magic = floor(2^32 / nn) + 1 */
+    /* gf_mod of the uint16 truncation of v */
+    __device__ __forceinline__ uint32_t operator()(uint32_t v) const
+    {
+        const uint32_t x = v & 0xffffu;
+        const uint32_t q = __umulhi(x, magic);
+        return x - q * nn;
+    }
+};
+
+/* LDS tables (768 B) + per-lane arrays [slot][index][lane] (bytes) */
+struct GShared {
+    uint8_t *alog, *log, *gen;
+    uint8_t *lane; /* start of the per-lane area */
+    uint32_t wg;
+    __device__ __forceinline__ uint8_t *arr(uint32_t slot, uint32_t nr1) const { return lane + slot * nr1 * wg; }
+};
+
+__device__ __forceinline__ GShared g_setup(const RsGenTables *__restrict__ T, uint8_t *smem)
+{
+    GShared s;
+    s.alog = smem;
+    s.log = smem + 256;
+    s.gen = smem + 512;
+    s.lane = smem + 768;
+    s.wg = blockDim.x;
+    for (uint32_t t = threadIdx.x; t < 768u; t += blockDim.x)
+        smem[t] = t < 256u ? T->alog[t] : (t < 512u ? T->log[t - 256u] : T->gen[t - 512u]);
+    __syncthreads();
+    return s;
+}
+
+/* per-lane view of one LDS array: element i of this lane */
+struct LaneArr {
+    uint8_t *p;
+    uint32_t wg;
+    __device__ __forceinline__ uint8_t &operator[](uint32_t i) const { return p[i * wg]; }
+};
+
+/* ------------------------------------------------------------------------ */
+/* encode, src/encode.c:120-143                                             */
+/* ------------------------------------------------------------------------ */
+
+/* The shift register is a ring in LDS: logical byte j is physical
+ * (head + j) mod nr, so the reference's memmove is a head increment. */
+__global__ __launch_bounds__(G_WG_MAX) void rsg_encode_k(const RsGenTables *__restrict__ T, RsGenParams P,
+                                                          const uint8_t *__restrict__ data, size_t dstride,
+                                                          uint8_t *__restrict__ parity, size_t pstride, size_t count)
+{
+    extern __shared__ uint8_t smem[];
+    const GShared s = g_setup(T, smem);
+    const GMod mod{P.nn, P.magic};
+    const uint32_t nr = P.nroots, A0 = P.nn;
+    const LaneArr reg{s.arr(0, nr + 1u) + threadIdx.x, s.wg};
+    for (size_t cw = (size_t)blockIdx.x * blockDim.x + threadIdx.x; cw < count;
+         cw += (size_t)gridDim.x * blockDim.x) {
+        const uint8_t *d = data + cw * dstride;
+        for (uint32_t j = 0; j < nr; ++j)
+            reg[j] = 0;
+        uint32_t head = 0;
+        for (uint32_t b = 0; b < P.size; ++b) {
+            const uint32_t fb = s.log[((uint32_t)d[b] & A0) ^ reg[head]];
+            if (fb != A0) {
+                uint32_t ph = head;
+                for (uint32_t j = 1; j < nr; ++j) {
+                    ph = ph + 1u == nr ? 0u : ph + 1u;
+                    reg[ph] = (uint8_t)(reg[ph] ^ s.alog[mod(fb + s.gen[nr - j])]);
+                }
+            }
+            /* shift: the old head slot becomes logical byte nr-1 */
+            reg[head] = fb != A0 ? s.alog[mod(fb + s.gen[0])] : (uint8_t)0;
+            head = head + 1u == nr ? 0u : head + 1u;
+        }
+        uint8_t *p = parity + cw * pstride;
+        for (uint32_t j = 0, ph = head; j < nr; ++j, ph = ph + 1u == nr ? 0u : ph + 1u)
+            p[j] = reg[ph];
+    }
+}
+
+/* ------------------------------------------------------------------------ */
+/* syndromes, src/decode.c:375-415 (log form out; returns the nonzero flag) */
+/* ------------------------------------------------------------------------ */
+
+__device__ __forceinline__ bool g_syndromes(const GShared &s, const GMod &mod, const RsGenParams &P,
+                                            const uint8_t *d, const uint8_t *par, const LaneArr &S)
+{
+    const uint32_t nr = P.nroots, A0 = P.nn;
+    const uint32_t first = (uint32_t)d[0] & A0;
+    for (uint32_t i = 0; i < nr; ++i)
+        S[i] = (uint8_t)first;
+    const uint32_t total = P.size + nr;
+    for (uint32_t b = 1; b < total; ++b) {
+        const uint32_t in = (uint32_t)(b < P.size ? d[b] : par[b - P.size]) & A0;
+        /* (fcr + i) * prim, as the reference's int arithmetic before the
+         * uint16 truncation inside gf_mod */
+        uint32_t step = P.fcr * P.prim;
+        for (uint32_t i = 0; i < nr; ++i, step += P.prim) {
+            const uint32_t v = S[i];
+            S[i] = (uint8_t)(v ? (in ^ s.alog[mod((uint32_t)s.log[v] + step)]) : in);
+        }
+    }
+    uint32_t flag = 0;
+    for (uint32_t i = 0; i < nr; ++i) {
+        const uint32_t v = S[i];
+        flag |= v;
+        S[i] = s.log[v];
+    }
+    return flag != 0;
+}
+
+/* ------------------------------------------------------------------------ */
+/* correction, src/decode.c:17-230                                          */
+/* ------------------------------------------------------------------------ */
+
+template <typename PosT>
+__device__ bool g_correct(const GShared &s, const GMod &mod, const RsGenParams &P, uint8_t *data, uint8_t *parity,
+                          const LaneArr &S, uint32_t ne, const PosT *pos, bool eras_apply, uint32_t &corrected)
+{
+    const uint32_t nr = P.nroots, A0 = P.nn, nr1 = nr + 1u;
+    const int32_t pad = P.pad;
+    const uint32_t t = threadIdx.x;
+    const LaneArr lam{s.arr(1, nr1) + t, s.wg}, B{s.arr(2, nr1) + t, s.wg}, om{s.arr(3, nr1) + t, s.wg};
+    const LaneArr roots{s.arr(4, nr1) + t, s.wg}, locs{s.arr(5, nr1) + t, s.wg}, mag{s.arr(6, nr1) + t, s.wg};
+    const uint8_t *alog = s.alog, *lg = s.log;
+
+    /* erasure locator prod(1 + X_l x), X_l = alpha^(prim (nn-1-(pos+pad))), src/decode.c:31-47 */
+    for (uint32_t i = 0; i <= nr; ++i)
+        lam[i] = 0;
+    lam[0] = 1;
+    if (ne > 0) {
+        lam[1] = alog[mod(P.prim * (A0 - 1u - ((uint32_t)pos[0] + (uint32_t)pad)))];
+        for (uint32_t i = 1; i < ne; ++i) {
+            const uint32_t xl = mod(P.prim * (A0 - 1u - ((uint32_t)pos[i] + (uint32_t)pad)));
+            for (uint32_t j = i + 1u; j > 0u; --j) {
+                const uint32_t l = lg[lam[j - 1u]];
+                if (l != A0)
+                    lam[j] = (uint8_t)(lam[j] ^ alog[mod(xl + l)]);
+            }
+        }
+    }
+    for (uint32_t i = 0; i <= nr; ++i)
+        B[i] = lg[lam[i]];
+
+    /* Berlekamp-Massey (Karn's form with erasures), src/decode.c:49-96.
+     * One top-down pass per iteration updates Lambda in place (it reads B
+     * at i-1 before that slot is rewritten) and builds the new B from the
+     * old Lambda, so no temporary polynomial is needed. */
+    uint32_t L = ne;
+    for (uint32_t r = ne + 1u; r <= nr; ++r) {
+        uint32_t disc = 0;
+        for (uint32_t i = 0; i < r; ++i) {
+            const uint32_t li = lam[i], si = S[r - i - 1u];
+            if (li != 0u && si != A0)
+                disc ^= alog[mod((uint32_t)lg[li] + si)];
+        }
+        disc = lg[disc];
+        if (disc == A0) {
+            for (uint32_t i = nr; i > 0u; --i)
+                B[i] = B[i - 1u];
+            B[0] = (uint8_t)A0;
+            continue;
+        }
+        const bool lengthen = 2u * L <= r + ne - 1u;
+        for (uint32_t i = nr + 1u; i-- > 0u;) {
+            const uint32_t old = lam[i];
+            if (i > 0u) {
+                const uint32_t b = B[i - 1u];
+                if (b != A0)
+                    lam[i] = (uint8_t)(old ^ alog[mod(disc + b)]);
+            }
+            if (lengthen)
+                B[i] = (uint8_t)(old == 0u ? A0 : mod((uint32_t)lg[old] - disc + A0));
+            else
+                B[i] = i > 0u ? B[i - 1u] : (uint8_t)A0;
+        }
+        if (lengthen)
+            L = r + ne - L;
+    }
+
+    /* locator to log form, degree, src/decode.c:98-110 */
+    uint32_t deg = 0;
+    for (uint32_t i = 0; i <= nr; ++i) {
+        const uint32_t l = lg[lam[i]];
+        lam[i] = (uint8_t)l;
+        if (l != A0)
+            deg = i;
+    }
+    if (deg == 0)
+        return false;
+
+    /* Chien search, src/decode.c:112-145; B is the register copy */
+    for (uint32_t j = 1; j <= nr; ++j)
+        B[j] = lam[j];
+    uint32_t cnt = 0;
+    {
+        int32_t k = (int16_t)(uint16_t)(P.iprim - 1u);
+        for (uint32_t i = 1; i <= A0; ++i, k = (int16_t)mod((uint32_t)(k + (int32_t)P.iprim))) {
+            uint32_t acc = 1;
+            for (uint32_t j = deg; j > 0u; --j) {
+                const uint32_t rj = B[j];
+                if (rj != A0) {
+                    const uint32_t v = mod(rj + j);
+                    B[j] = (uint8_t)v;
+                    acc ^= alog[v];
+                }
+            }
+            if (acc != 0u)
+                continue;
+            if (k < pad)
+                return false;
+            roots[cnt] = (uint8_t)i;
+            locs[cnt] = (uint8_t)k;
+            if (++cnt == deg)
+                break;
+        }
+    }
+    if (cnt != deg)
+        return false;
+
+    /* Omega = S Lambda mod x^deg, log form, src/decode.c:147-158 */
+    for (uint32_t i = 0; i < deg; ++i) {
+        uint32_t acc = 0;
+        for (uint32_t j = 0; j <= i; ++j) {
+            const uint32_t sv = S[i - j], lv = lam[j];
+            if (sv != A0 && lv != A0)
+                acc ^= alog[mod(sv + lv)];
+        }
+        om[i] = lg[acc];
+    }
+
+    /* Forney, src/decode.c:159-191 (corrected counts nonzero numerators) */
+    corrected = 0;
+    const uint32_t dtop = (deg < nr - 1u ? deg : nr - 1u) & ~1u;
+    for (uint32_t jj = cnt; jj-- > 0u;) {
+        const uint32_t rt = roots[jj];
+        uint32_t num = 0;
+        for (uint32_t i = 0; i < deg; ++i) {
+            const uint32_t o = om[i];
+            if (o != A0)
+                num ^= alog[mod(o + i * rt)];
+        }
+        if (num == 0u) {
+            mag[jj] = 0;
+            continue;
+        }
+        const uint32_t num2 = alog[mod((uint32_t)((int32_t)rt * ((int32_t)P.fcr - 1) + (int32_t)A0))];
+        uint32_t den = 0;
+        for (int32_t i = (int32_t)dtop; i >= 0; i -= 2) {
+            const uint32_t l1 = lam[(uint32_t)i + 1u];
+            if (l1 != A0)
+                den ^= alog[mod(l1 + (uint32_t)i * rt)];
+        }
+        mag[jj] = alog[mod((uint32_t)lg[num] + lg[num2] + A0 - lg[den])];
+        ++corrected;
+    }
+
+    /* re-syndrome check, src/decode.c:193-209 (int16 exponent) */
+    for (uint32_t i = 0; i < nr; ++i) {
+        uint32_t acc = 0;
+        for (uint32_t j = 0; j < cnt; ++j) {
+            const uint32_t mj = mag[j];
+            if (mj == 0u)
+                continue;
+            const int32_t kk = (int16_t)(uint16_t)((P.fcr + i) * P.prim * (A0 - (uint32_t)locs[j] - 1u));
+            acc ^= alog[mod((uint32_t)((int32_t)lg[mj] + kk))];
+        }
+        if (acc != alog[S[i]])
+            return false;
+    }
+
+    /* apply, src/decode.c:211-227 */
+    if (eras_apply) {
+        /* quirk Q1/Q2: magnitude j (ascending location) goes to list slot j;
+         * slots past data[] address parity (p < size + nr) or are dropped */
+        for (uint32_t i = 0; i < cnt; ++i) {
+            const uint32_t p = (uint32_t)pos[i];
+            if (p < P.size)
+                data[p] ^= mag[i];
+            else if (p < P.size + nr)
+                parity[p - P.size] ^= mag[i];
+        }
+    } else {
+        for (uint32_t i = 0; i < cnt; ++i) {
+            const int32_t p = (int32_t)locs[i] - pad;
+            if (p >= 0 && p < (int32_t)P.size)
+                data[p] ^= mag[i];
+            else if (p >= (int32_t)P.size && p < (int32_t)(P.size + nr))
+                parity[p - (int32_t)P.size] ^= mag[i];
+            else
+                return false;
+        }
+    }
+    return true;
+}
+
+/* Full decode of one batch: branch logic of src/decode.c:431-487.
+ * ext: external log-form syndromes (nroots u16 per codeword at ext_stride),
+ * values > nn refuse the codeword (out-of-table in the reference).
+ * pos/cnt: erasure lists (erasure-object mode), counts > nroots refused. */
+template <typename PosT>
+__global__ __launch_bounds__(G_WG_MAX) void rsg_decode_k(const RsGenTables *__restrict__ T, RsGenParams P,
+                                                          uint8_t *data, size_t dstride, uint8_t *parity,
+                                                          size_t pstride, size_t count,
+                                                          const uint16_t *__restrict__ ext, size_t ext_stride,
+                                                          const PosT *__restrict__ pos, size_t pos_stride,
+                                                          const uint8_t *__restrict__ cntv, uint8_t *__restrict__ ok,
+                                                          uint8_t *__restrict__ corrected)
+{
+    extern __shared__ uint8_t smem[];
+    const GShared s = g_setup(T, smem);
+    const GMod mod{P.nn, P.magic};
+    const uint32_t nr = P.nroots, A0 = P.nn;
+    const LaneArr S{s.arr(0, nr + 1u) + threadIdx.x, s.wg};
+    for (size_t cw = (size_t)blockIdx.x * blockDim.x + threadIdx.x; cw < count;
+         cw += (size_t)gridDim.x * blockDim.x) {
+        uint8_t *d = data + cw * dstride;
+        uint8_t *par = parity + cw * pstride;
+        uint32_t fixed = 0;
+        bool good;
+        if (ext) {
+            const uint16_t *e = ext + cw * ext_stride;
+            bool any = false, bad = false;
+            for (uint32_t i = 0; i < nr; ++i) {
+                const uint32_t v = e[i];
+                bad |= v > A0;
+                any |= v != A0;
+                S[i] = (uint8_t)v;
+            }
+            good = !bad && (!any || g_correct<PosT>(s, mod, P, d, par, S, 0u, (const PosT *)nullptr, false, fixed));
+            if (bad)
+                fixed = 0;
+        } else if (pos) {
+            const uint32_t ne = cntv[cw];
+            if (ne > nr) { /* quirk Q5: overflows the locator in the reference */
+                good = false;
+            } else {
+                good = !g_syndromes(s, mod, P, d, par, S) ||
+                       g_correct<PosT>(s, mod, P, d, par, S, ne, pos + cw * pos_stride, true, fixed);
+            }
+        } else {
+            good = !g_syndromes(s, mod, P, d, par, S) ||
+                   g_correct<PosT>(s, mod, P, d, par, S, 0u, (const PosT *)nullptr, false, fixed);
+        }
+        ok[cw] = good ? 1 : 0;
+        if (corrected)
+            corrected[cw] = (uint8_t)fixed;
+    }
+}
+
+__global__ __launch_bounds__(G_WG_MAX) void rsg_check_k(const RsGenTables *__restrict__ T, RsGenParams P,
+                                                         const uint8_t *__restrict__ data, size_t dstride,
+                                                         const uint8_t *__restrict__ parity, size_t pstride,
+                                                         size_t count, uint8_t *__restrict__ dirty)
+{
+    extern __shared__ uint8_t smem[];
+    const GShared s = g_setup(T, smem);
+    const GMod mod{P.nn, P.magic};
+    const LaneArr S{s.arr(0, P.nroots + 1u) + threadIdx.x, s.wg};
+    for (size_t cw = (size_t)blockIdx.x * blockDim.x + threadIdx.x; cw < count;
+         cw += (size_t)gridDim.x * blockDim.x)
+        dirty[cw] = g_syndromes(s, mod, P, data + cw * dstride, parity + cw * pstride, S) ? 1 : 0;
+}
+
+/* ------------------------------------------------------------------------ */
+/* launchers                                                                */
+/* ------------------------------------------------------------------------ */
+
+/* workgroup size and LDS bytes for `slots` per-lane arrays of nroots+1 bytes */
+static void g_shape(const RsGenParams &P, uint32_t slots, uint32_t &wg, size_t &lds)
+{
+    const size_t per_lane = (size_t)slots * (P.nroots + 1u);
+    wg = G_WG_MAX;
+    while (wg > 64u && 768u + per_lane * wg > 64u * 1024u)
+        wg -= 64u;
+    lds = 768u + per_lane * wg;
+}
+
+static dim3 g_grid(size_t count, uint32_t wg, int num_cu, size_t lds)
+{
+    const size_t per_cu = std::max<size_t>(1, std::min<size_t>(8, (160u * 1024u) / lds));
+    const size_t need = (count + wg - 1) / wg;
+    const size_t cap = (size_t)(num_cu > 0 ? num_cu : 256) * per_cu;
+    return dim3((uint32_t)std::max<size_t>(1, std::min(need, cap)));
+}
+
+extern "C" hipError_t rsg_encode(const RsGenTables *tab, const RsGenParams *prm, const uint8_t *data, size_t dstride,
+                                 uint8_t *parity, size_t pstride, size_t count, int num_cu, hipStream_t stream)
+{
+    if (count == 0)
+        return hipSuccess;
+    uint32_t wg;
+    size_t lds;
+    g_shape(*prm, 1, wg, lds);
+    hipLaunchKernelGGL(rsg_encode_k, g_grid(count, wg, num_cu, lds), dim3(wg), lds, stream, tab, *prm, data, dstride,
+                       parity, pstride, count);
+    return hipGetLastError();
+}
+
+extern "C" hipError_t rsg_decode(const RsGenTables *tab, const RsGenParams *prm, uint8_t *data, size_t dstride,
+                                 uint8_t *parity, size_t pstride, size_t count, const uint16_t *ext,
+                                 size_t ext_stride, const uint8_t *pos8, const uint32_t *pos32, size_t pos_stride,
+                                 const uint8_t *cnt, uint8_t *ok, uint8_t *corrected, int num_cu, hipStream_t stream)
+{
+    if (count == 0)
+        return hipSuccess;
+    uint32_t wg;
+    size_t lds;
+    g_shape(*prm, 7, wg, lds);
+    const dim3 grid = g_grid(count, wg, num_cu, lds);
+    if (pos32)
+        hipLaunchKernelGGL(rsg_decode_k<uint32_t>, grid, dim3(wg), lds, stream, tab, *prm, data, dstride, parity,
+                           pstride, count, ext, ext_stride, pos32, pos_stride, cnt, ok, corrected);
+    else
+        hipLaunchKernelGGL(rsg_decode_k<uint8_t>, grid, dim3(wg), lds, stream, tab, *prm, data, dstride, parity,
+                           pstride, count, ext, ext_stride, pos8, pos_stride, cnt, ok, corrected);
+    return hipGetLastError();
+}
+
+extern "C" hipError_t rsg_check(const RsGenTables *tab, const RsGenParams *prm, const uint8_t *data, size_t dstride,
+                                const uint8_t *parity, size_t pstride, size_t count, uint8_t *dirty, int num_cu,
+                                hipStream_t stream)
+{
+    if (count == 0)
+        return hipSuccess;
+    uint32_t wg;
+    size_t lds;
+    g_shape(*prm, 1, wg, lds);
+    hipLaunchKernelGGL(rsg_check_k, g_grid(count, wg, num_cu, lds), dim3(wg), lds, stream, tab, *prm, data, dstride,
+                       parity, pstride, count, dirty);
+    return hipGetLastError();
+}

@@ -65,7 +65,10 @@ def test_rs_handle_getters():
     assert h.supported
     h16 = P.Poporon(8, 0x11D, 1, 1, 16)
     assert h16.parity_size == 16 and h16.info_size == 239
-    assert not h16.supported  # the GPU kernels serve num_roots == 32
+    assert h16.supported  # general-parameter kernels (rs_generic.hip)
+    assert P.Poporon(4, 0x13, 1, 2, 8).supported
+    assert P.Poporon(2, 0x7, 1, 1, 2).supported
+    assert not P.Poporon(1, 0x3, 1, 1, 0).supported  # GF(2): no byte-symbol RS code to serve
     with pytest.raises(P.PoporonError):
         P.Poporon(8, 0x11C, 1, 1, 32)  # non-primitive field polynomial -> NULL
     with pytest.raises(P.PoporonError):
@@ -139,3 +142,23 @@ def test_shard_range_partitions():
             got = [P.shard_range(count, r, world) for r in range(world)]
             assert got[0][0] == 0 and got[-1][1] == count
             assert all(got[i][1] == got[i + 1][0] for i in range(world - 1))
+
+
+def test_gf_mod_is_uint16_modulo():
+    """rs_generic.hip computes gf_mod (src/internal/common.h:102-110) as
+    (v mod 2^16) mod (2^m - 1) with a reciprocal multiply: check both claims
+    for every uint16 argument and every byte symbol size."""
+    v = np.arange(1 << 16, dtype=np.uint64)
+    for m in range(2, 9):
+        nn = (1 << m) - 1
+        x = v.copy()
+        while True:  # the reference's folding loop, vectorised
+            big = x >= nn
+            if not big.any():
+                break
+            y = (x[big] - nn) & 0xFFFF
+            x[big] = ((y >> m) + (y & nn)) & 0xFFFF
+        assert (x == v % nn).all(), m
+        magic = (1 << 32) // nn + 1
+        q = (v * magic) >> 32
+        assert (v - q * nn == v % nn).all(), m

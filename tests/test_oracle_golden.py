@@ -136,3 +136,36 @@ def test_restatement_vs_reference_random():
         cw[pos] ^= rng.integers(1, 256, ne, dtype=np.uint8)
         a, b = o.decode(cw[:size], cw[size:]), r.decode(cw[:size], cw[size:])
         assert a[0] == b[0] and a[1] == b[1] and (a[2] == b[2]).all() and (a[3] == b[3]).all()
+
+
+# ---------------------------------------------------------------------------
+# general parameters (tests/golden/rs_params_golden.npz, tools/gen_golden_params.py)
+# ---------------------------------------------------------------------------
+PARAMS_GOLDEN = __import__("os").path.join(__import__("os").path.dirname(__file__), "golden", "rs_params_golden.npz")
+
+
+@pytest.fixture(scope="module")
+def pgolden():
+    return np.load(PARAMS_GOLDEN)
+
+
+@pytest.mark.parametrize("gi", range(13))
+def test_oracle_general_parameters_golden(pgolden, gi):
+    m, poly, fcr, prim, nr = (int(x) for x in pgolden["params"][gi])
+    o = Oracle(m, poly, fcr, prim, nr)
+    g = lambda k: pgolden[f"g{gi}_{k}"]  # noqa: E731
+    for s, d, p in zip(g("enc_size"), g("enc_data"), g("enc_parity")):
+        assert (o.encode(d[:s]) == p).all()
+    for s, inp, out, ok, cor in zip(g("dec_size"), g("dec_in"), g("dec_out"), g("dec_ok"), g("dec_cor")):
+        s = int(s)
+        gok, gn, gd, gp = o.decode(inp[:s], inp[s:s + nr])
+        assert gok == bool(ok) and gn == cor and (np.concatenate([gd, gp]) == out[:s + nr]).all()
+    for s, e, slots, inp, out, ok, cor in zip(g("era_size"), g("era_count"), g("era_slots"), g("era_in"),
+                                              g("era_out"), g("era_ok"), g("era_cor")):
+        s, e = int(s), int(e)
+        gok, gn, gd, gp = o.decode(inp[:s], inp[s:s + nr], erasures=slots[:e])
+        assert gok == bool(ok) and gn == cor and (np.concatenate([gd, gp]) == out[:s + nr]).all()
+    k = (1 << m) - 1 - nr
+    for syn, inp, out, ok, cor in zip(g("xs_syn"), g("xs_in"), g("xs_out"), g("xs_ok"), g("xs_cor")):
+        gok, gn, gd, gp = o.decode(inp[:k], inp[k:k + nr], ext_syn=syn)
+        assert gok == bool(ok) and gn == cor and (np.concatenate([gd, gp]) == out[:k + nr]).all()
