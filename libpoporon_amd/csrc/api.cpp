@@ -23,6 +23,7 @@
 #include <cstring>
 #include <new>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "poporon.h"
@@ -122,10 +123,21 @@ struct GpuCtx {
     RsGenTables *gtab = nullptr; /* device (general-parameter kernels) */
     uint8_t *rem = nullptr;     /* device workspace: 32 B per codeword */
     size_t rem_cap = 0;
-    /* single-codeword / host-batch staging (device) */
+    /* single-codeword staging (device) */
     uint8_t *stage = nullptr;
     size_t stage_cap = 0;
+    /* host-batch pipeline: PIPE_SLOTS chunks in flight, one stream each */
+    struct PipeSlot {
+        hipStream_t stream = nullptr;
+        hipEvent_t done = nullptr;
+        uint8_t *host = nullptr; /* pinned */
+        uint8_t *dev = nullptr;
+        size_t cap = 0;
+        bool busy = false;
+        size_t c0 = 0, n = 0; /* the chunk whose results the slot holds */
+    } pipe[3];
 };
+#define PIPE_SLOTS 3
 
 struct _poporon_t {
     poporon_fec_type_t fec_type;
@@ -573,6 +585,16 @@ static void gpu_release(GpuCtx &g)
     (void)hipFree(g.gtab);
     (void)hipFree(g.rem);
     (void)hipFree(g.stage);
+    for (auto &ps : g.pipe) {
+        if (ps.stream)
+            (void)hipStreamSynchronize(ps.stream);
+        (void)hipHostFree(ps.host);
+        (void)hipFree(ps.dev);
+        if (ps.done)
+            (void)hipEventDestroy(ps.done);
+        if (ps.stream)
+            (void)hipStreamDestroy(ps.stream);
+    }
     if (g.stream)
         (void)hipStreamDestroy(g.stream);
     if (prev >= 0)
@@ -840,7 +862,7 @@ static bool launch_encode(poporon_t *h, const uint8_t *d_data, size_t ds, uint8_
 static bool launch_decode(poporon_t *h, uint8_t *d_data, size_t ds, uint8_t *d_par, size_t ps, size_t size,
                           size_t count, const uint16_t *ext_syn, size_t ext_stride, const uint8_t *pos8,
                           const uint32_t *pos32, size_t pos_stride, const uint8_t *cnt, uint8_t *ok,
-                          uint8_t *corrected, hipStream_t s)
+                          uint8_t *corrected, hipStream_t s, uint8_t *rem = nullptr)
 {
     if (!h->fast) {
         RsGenParams prm = h->gen;
@@ -855,15 +877,18 @@ static bool launch_decode(poporon_t *h, uint8_t *d_data, size_t ds, uint8_t *d_p
     RsCorrParams prm = h->corr;
     prm.size = (uint32_t)size;
     prm.pad = (int32_t)(h->rs->gf->field_size - h->rs->num_roots - size);
-    if (!ext_syn) {
-        if (!ensure_rem(h, count))
+    if (!rem) {
+        if (!ext_syn && !ensure_rem(h, count))
             return false;
+        rem = h->gpu.rem;
+    }
+    if (!ext_syn) {
         KernelTimer t(h->gpu, POPORON_AMD_KERNEL_REMAINDER, s);
-        HIP_OK(rsk_syndrome(h->gpu.tab, d_data, ds, d_par, ps, (uint32_t)size, count, h->gpu.rem, h->gpu.num_cu, s));
+        HIP_OK(rsk_syndrome(h->gpu.tab, d_data, ds, d_par, ps, (uint32_t)size, count, rem, h->gpu.num_cu, s));
         t.done();
     }
     KernelTimer t(h->gpu, POPORON_AMD_KERNEL_CORRECT, s);
-    HIP_OK(rsk_correct(h->gpu.tab, &prm, d_data, ds, d_par, ps, count, h->gpu.rem, ext_syn, ext_stride, pos8, pos32,
+    HIP_OK(rsk_correct(h->gpu.tab, &prm, d_data, ds, d_par, ps, count, rem, ext_syn, ext_stride, pos8, pos32,
                        pos_stride, cnt, ok, corrected, h->gpu.num_cu, s));
     t.done();
     return true;
@@ -948,26 +973,76 @@ EXPORT bool poporon_decode_batch_syndrome_device(poporon_t *h, uint8_t *d_data, 
 /* host batches: staged through device memory in chunks                     */
 /* ------------------------------------------------------------------------ */
 
-static const size_t kHostChunk = 1u << 20; /* codewords per staged chunk */
+/*
+ * Host batches are streamed through PIPE_SLOTS slots, each with its own HIP
+ * stream, pinned host buffer and device buffer.  Chunk i goes to slot
+ * i % PIPE_SLOTS: its rows are gathered into pinned memory (CPU threads),
+ * copied in, processed and copied back asynchronously; the slot's results are
+ * scattered to the caller's arrays only when the slot is needed again (or at
+ * the end).  So the CPU gather of chunk i+1, the H2D copy of chunk i+1, the
+ * kernels of chunk i and the D2H copy of chunk i-1 overlap.
+ */
+static const size_t kPipeChunk = 1u << 18; /* codewords per chunk */
 
-static void gather(uint8_t *dst, const uint8_t *src, size_t stride, size_t width, size_t count)
+/* row copy dst[c*dw .. +w) = src[c*sw .. +w) for c < count, split over CPU threads */
+static void copy_rows(uint8_t *dst, size_t dw, const uint8_t *src, size_t sw, size_t w, size_t count)
 {
-    if (stride == width) {
-        memcpy(dst, src, width * count);
+    auto run = [=](size_t a, size_t b) {
+        if (dw == w && sw == w) {
+            memcpy(dst + a * w, src + a * w, (b - a) * w);
+            return;
+        }
+        for (size_t c = a; c < b; c++)
+            memcpy(dst + c * dw, src + c * sw, w);
+    };
+    const size_t bytes = w * count;
+    unsigned nt = std::thread::hardware_concurrency();
+    nt = std::max(1u, std::min(nt, 8u));
+    if (bytes < (4u << 20) || nt == 1) {
+        run(0, count);
         return;
     }
-    for (size_t c = 0; c < count; c++)
-        memcpy(dst + c * width, src + c * stride, width);
+    std::vector<std::thread> th;
+    const size_t per = (count + nt - 1) / nt;
+    for (unsigned t = 1; t < nt; t++) {
+        const size_t a = std::min(count, t * per), b = std::min(count, a + per);
+        if (a < b)
+            th.emplace_back(run, a, b);
+    }
+    run(0, std::min(count, per));
+    for (auto &x : th)
+        x.join();
 }
 
-static void scatter(uint8_t *dst, size_t stride, const uint8_t *src, size_t width, size_t count)
+static bool pipe_slot(poporon_t *h, GpuCtx::PipeSlot &ps, size_t bytes)
 {
-    if (stride == width) {
-        memcpy(dst, src, width * count);
-        return;
+    if (!ps.stream)
+        HIP_OK(hipStreamCreateWithFlags(&ps.stream, hipStreamNonBlocking));
+    if (!ps.done)
+        HIP_OK(hipEventCreateWithFlags(&ps.done, hipEventDisableTiming));
+    if (ps.cap >= bytes)
+        return true;
+    HIP_OK(hipStreamSynchronize(ps.stream));
+    (void)hipHostFree(ps.host);
+    (void)hipFree(ps.dev);
+    ps.host = nullptr;
+    ps.dev = nullptr;
+    ps.cap = 0;
+    HIP_OK(hipHostMalloc((void **)&ps.host, bytes, hipHostMallocDefault));
+    HIP_OK(hipMalloc((void **)&ps.dev, bytes));
+    ps.cap = bytes;
+    return true;
+}
+
+/* wait for every slot (after an error: nothing may still be in flight into
+ * the pinned buffers) */
+static void pipe_drain(GpuCtx &g)
+{
+    for (auto &ps : g.pipe) {
+        if (ps.stream)
+            (void)hipStreamSynchronize(ps.stream);
+        ps.busy = false;
     }
-    for (size_t c = 0; c < count; c++)
-        memcpy(dst + c * stride, src + c * width, width);
 }
 
 EXPORT bool poporon_encode_batch(poporon_t *h, const uint8_t *data, size_t data_stride, uint8_t *parity,
@@ -982,20 +1057,42 @@ EXPORT bool poporon_encode_batch(poporon_t *h, const uint8_t *data, size_t data_
     DeviceGuard dg(h->gpu.device);
     GpuCtx &g = h->gpu;
     const size_t nr = h->rs->num_roots;
-    const size_t chunk = std::min(count, kHostChunk);
-    if (!ensure_stage(h, chunk * (size + nr) + 16))
-        return false;
-    std::vector<uint8_t> tmp(chunk * (size + nr));
-    for (size_t c0 = 0; c0 < count; c0 += chunk) {
-        const size_t n = std::min(chunk, count - c0);
-        gather(tmp.data(), data + c0 * data_stride, data_stride, size, n);
-        uint8_t *dd = g.stage, *dp = g.stage + n * size;
-        HIP_OK(hipMemcpyAsync(dd, tmp.data(), n * size, hipMemcpyHostToDevice, g.stream));
-        if (!launch_encode(h, dd, size, dp, nr, size, n, g.stream))
+    const size_t chunk = std::max<size_t>(1, std::min(count, kPipeChunk));
+    for (auto &ps : g.pipe)
+        if (!pipe_slot(h, ps, chunk * (size + nr) + 64))
             return false;
-        HIP_OK(hipMemcpyAsync(tmp.data(), dp, n * nr, hipMemcpyDeviceToHost, g.stream));
-        HIP_OK(hipStreamSynchronize(g.stream));
-        scatter(parity + c0 * parity_stride, parity_stride, tmp.data(), nr, n);
+    /* parity of the slot's chunk -> caller */
+    auto finish = [&](GpuCtx::PipeSlot &ps) -> bool {
+        if (!ps.busy)
+            return true;
+        ps.busy = false;
+        HIP_OK(hipEventSynchronize(ps.done));
+        copy_rows(parity + ps.c0 * parity_stride, parity_stride, ps.host + ps.n * size, nr, nr, ps.n);
+        return true;
+    };
+    bool ok = true;
+    size_t i = 0;
+    for (size_t c0 = 0; ok && c0 < count; c0 += chunk, i++) {
+        GpuCtx::PipeSlot &ps = g.pipe[i % PIPE_SLOTS];
+        if (!(ok = finish(ps)))
+            break;
+        const size_t n = std::min(chunk, count - c0);
+        uint8_t *hd = ps.host, *dd = ps.dev, *dp = ps.dev + n * size;
+        copy_rows(hd, size, data + c0 * data_stride, data_stride, size, n);
+        ok = hipMemcpyAsync(dd, hd, n * size, hipMemcpyHostToDevice, ps.stream) == hipSuccess &&
+             launch_encode(h, dd, size, dp, nr, size, n, ps.stream) &&
+             hipMemcpyAsync(hd + n * size, dp, n * nr, hipMemcpyDeviceToHost, ps.stream) == hipSuccess &&
+             hipEventRecord(ps.done, ps.stream) == hipSuccess;
+        ps.busy = true;
+        ps.c0 = c0;
+        ps.n = n;
+    }
+    for (size_t k = 0; ok && k < PIPE_SLOTS; k++) /* oldest first */
+        ok = finish(g.pipe[(i + k) % PIPE_SLOTS]);
+    if (!ok) {
+        const std::string msg = g_last_error.empty() ? std::string("HIP failure in the host pipeline") : g_last_error;
+        pipe_drain(g);
+        return fail("%s", msg.c_str());
     }
     return true;
 }
@@ -1015,35 +1112,61 @@ EXPORT bool poporon_decode_batch(poporon_t *h, uint8_t *data, size_t data_stride
     DeviceGuard dg(h->gpu.device);
     GpuCtx &g = h->gpu;
     const size_t nr = h->rs->num_roots;
-    const size_t chunk = std::min(count, kHostChunk);
-    const size_t per = size + nr + 2 + (positions ? nr + 1 : 0);
-    if (!ensure_stage(h, chunk * per + 64))
-        return false;
-    std::vector<uint8_t> tmp(chunk * (size + nr));
-    for (size_t c0 = 0; c0 < count; c0 += chunk) {
-        const size_t n = std::min(chunk, count - c0);
-        uint8_t *dd = g.stage, *dp = dd + n * size, *dok = dp + n * nr, *dcor = dok + n, *dpos = dcor + n,
-                *dcnt = dpos + (positions ? n * nr : 0);
-        gather(tmp.data(), data + c0 * data_stride, data_stride, size, n);
-        gather(tmp.data() + n * size, parity + c0 * parity_stride, parity_stride, nr, n);
-        HIP_OK(hipMemcpyAsync(dd, tmp.data(), n * (size + nr), hipMemcpyHostToDevice, g.stream));
-        if (positions) {
-            std::vector<uint8_t> pt(n * nr);
-            gather(pt.data(), positions + c0 * positions_stride, positions_stride, nr, n);
-            HIP_OK(hipMemcpyAsync(dpos, pt.data(), n * nr, hipMemcpyHostToDevice, g.stream));
-            HIP_OK(hipMemcpyAsync(dcnt, counts + c0, n, hipMemcpyHostToDevice, g.stream));
-            HIP_OK(hipStreamSynchronize(g.stream));
-        }
-        if (!launch_decode(h, dd, size, dp, nr, size, n, nullptr, 0, positions ? dpos : nullptr, nullptr, nr,
-                           positions ? dcnt : nullptr, dok, dcor, g.stream))
+    const size_t w = size + nr;
+    const size_t chunk = std::max<size_t>(1, std::min(count, kPipeChunk));
+    /* slot layout: [codewords w*n | ok n | cor n | positions nr*n | counts n | syndrome workspace 32*n (device)] */
+    const size_t per = w + 2 + (positions ? nr + 1 : 0) + RS_NR;
+    for (auto &ps : g.pipe)
+        if (!pipe_slot(h, ps, chunk * per + 256))
             return false;
-        HIP_OK(hipMemcpyAsync(tmp.data(), dd, n * (size + nr), hipMemcpyDeviceToHost, g.stream));
-        HIP_OK(hipMemcpyAsync(ok + c0, dok, n, hipMemcpyDeviceToHost, g.stream));
+    auto finish = [&](GpuCtx::PipeSlot &ps) -> bool {
+        if (!ps.busy)
+            return true;
+        ps.busy = false;
+        HIP_OK(hipEventSynchronize(ps.done));
+        const size_t n = ps.n;
+        copy_rows(data + ps.c0 * data_stride, data_stride, ps.host, w, size, n);
+        copy_rows(parity + ps.c0 * parity_stride, parity_stride, ps.host + size, w, nr, n);
+        memcpy(ok + ps.c0, ps.host + n * w, n);
         if (corrected)
-            HIP_OK(hipMemcpyAsync(corrected + c0, dcor, n, hipMemcpyDeviceToHost, g.stream));
-        HIP_OK(hipStreamSynchronize(g.stream));
-        scatter(data + c0 * data_stride, data_stride, tmp.data(), size, n);
-        scatter(parity + c0 * parity_stride, parity_stride, tmp.data() + n * size, nr, n);
+            memcpy(corrected + ps.c0, ps.host + n * w + n, n);
+        return true;
+    };
+    bool good = true;
+    size_t i = 0;
+    for (size_t c0 = 0; good && c0 < count; c0 += chunk, i++) {
+        GpuCtx::PipeSlot &ps = g.pipe[i % PIPE_SLOTS];
+        if (!(good = finish(ps)))
+            break;
+        const size_t n = std::min(chunk, count - c0);
+        uint8_t *hc = ps.host, *dc = ps.dev;
+        const size_t o_ok = n * w, o_cor = o_ok + n, o_pos = o_cor + n, o_cnt = o_pos + (positions ? n * nr : 0);
+        const size_t o_rem = (o_cnt + (positions ? n : 0) + 255) & ~(size_t)255;
+        /* codeword rows [data | parity] */
+        copy_rows(hc, w, data + c0 * data_stride, data_stride, size, n);
+        copy_rows(hc + size, w, parity + c0 * parity_stride, parity_stride, nr, n);
+        size_t in_bytes = n * w;
+        if (positions) {
+            copy_rows(hc + o_pos, nr, positions + c0 * positions_stride, positions_stride, nr, n);
+            memcpy(hc + o_cnt, counts + c0, n);
+        }
+        good = hipMemcpyAsync(dc, hc, in_bytes, hipMemcpyHostToDevice, ps.stream) == hipSuccess &&
+               (!positions || hipMemcpyAsync(dc + o_pos, hc + o_pos, n * nr + n, hipMemcpyHostToDevice,
+                                             ps.stream) == hipSuccess) &&
+               launch_decode(h, dc, w, dc + size, w, size, n, nullptr, 0, positions ? dc + o_pos : nullptr, nullptr,
+                             nr, positions ? dc + o_cnt : nullptr, dc + o_ok, dc + o_cor, ps.stream, dc + o_rem) &&
+               hipMemcpyAsync(hc, dc, n * w + 2 * n, hipMemcpyDeviceToHost, ps.stream) == hipSuccess &&
+               hipEventRecord(ps.done, ps.stream) == hipSuccess;
+        ps.busy = true;
+        ps.c0 = c0;
+        ps.n = n;
+    }
+    for (size_t k = 0; good && k < PIPE_SLOTS; k++)
+        good = finish(g.pipe[(i + k) % PIPE_SLOTS]);
+    if (!good) {
+        const std::string msg = g_last_error.empty() ? std::string("HIP failure in the host pipeline") : g_last_error;
+        pipe_drain(g);
+        return fail("%s", msg.c_str());
     }
     return true;
 }
