@@ -997,7 +997,7 @@ static void copy_rows(uint8_t *dst, size_t dw, const uint8_t *src, size_t sw, si
     };
     const size_t bytes = w * count;
     unsigned nt = std::thread::hardware_concurrency();
-    nt = std::max(1u, std::min(nt, 8u));
+    nt = std::max(1u, std::min(nt, 16u));
     if (bytes < (4u << 20) || nt == 1) {
         run(0, count);
         return;
@@ -1116,6 +1116,8 @@ EXPORT bool poporon_decode_batch(poporon_t *h, uint8_t *data, size_t data_stride
     const size_t chunk = std::max<size_t>(1, std::min(count, kPipeChunk));
     /* slot layout: [codewords w*n | ok n | cor n | positions nr*n | counts n | syndrome workspace 32*n (device)] */
     const size_t per = w + 2 + (positions ? nr + 1 : 0) + RS_NR;
+    /* parity right after the data in rows of equal stride: move whole rows */
+    const bool rows = parity == data + size && parity_stride == data_stride;
     for (auto &ps : g.pipe)
         if (!pipe_slot(h, ps, chunk * per + 256))
             return false;
@@ -1125,8 +1127,12 @@ EXPORT bool poporon_decode_batch(poporon_t *h, uint8_t *data, size_t data_stride
         ps.busy = false;
         HIP_OK(hipEventSynchronize(ps.done));
         const size_t n = ps.n;
-        copy_rows(data + ps.c0 * data_stride, data_stride, ps.host, w, size, n);
-        copy_rows(parity + ps.c0 * parity_stride, parity_stride, ps.host + size, w, nr, n);
+        if (rows) { /* wire layout: whole codeword rows */
+            copy_rows(data + ps.c0 * data_stride, data_stride, ps.host, w, w, n);
+        } else {
+            copy_rows(data + ps.c0 * data_stride, data_stride, ps.host, w, size, n);
+            copy_rows(parity + ps.c0 * parity_stride, parity_stride, ps.host + size, w, nr, n);
+        }
         memcpy(ok + ps.c0, ps.host + n * w, n);
         if (corrected)
             memcpy(corrected + ps.c0, ps.host + n * w + n, n);
@@ -1143,8 +1149,12 @@ EXPORT bool poporon_decode_batch(poporon_t *h, uint8_t *data, size_t data_stride
         const size_t o_ok = n * w, o_cor = o_ok + n, o_pos = o_cor + n, o_cnt = o_pos + (positions ? n * nr : 0);
         const size_t o_rem = (o_cnt + (positions ? n : 0) + 255) & ~(size_t)255;
         /* codeword rows [data | parity] */
-        copy_rows(hc, w, data + c0 * data_stride, data_stride, size, n);
-        copy_rows(hc + size, w, parity + c0 * parity_stride, parity_stride, nr, n);
+        if (rows) {
+            copy_rows(hc, w, data + c0 * data_stride, data_stride, w, n);
+        } else {
+            copy_rows(hc, w, data + c0 * data_stride, data_stride, size, n);
+            copy_rows(hc + size, w, parity + c0 * parity_stride, parity_stride, nr, n);
+        }
         size_t in_bytes = n * w;
         if (positions) {
             copy_rows(hc + o_pos, nr, positions + c0 * positions_stride, positions_stride, nr, n);
