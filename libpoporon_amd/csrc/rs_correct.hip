@@ -17,13 +17,20 @@
  *                     (bytes 2-3)}, x < 512, replicated 32x so that lane l's
  *                     reads always hit bank l & 31 (conflict-free).
  *
- * Zero sentinel.  In registers the log of zero is ZL = 1024 (log16[0] = ZL),
- * and every valid log is reduced (< 255).  A product is exp(a + b): with
- * both logs valid a + b <= 508 indexes lgf; with either one a zero the index
- * is >= 512 and the address lies past the end of the workgroup's LDS
- * allocation, where gfx950 returns 0 (probed: tools/probes/lds_oob.hip,
- * profiles/r01_lds_oob_probe.log).  So GF multiply-accumulate needs no zero
- * tests: one add, one address, one ds_read_u8, one XOR.
+ * Zero sentinel.  In registers the log of zero is ZL = 1024 (or 511, as
+ * returned by the log table), and every valid log is reduced (< 255).  A
+ * product is exp(a + b): with both logs valid a + b <= 508 indexes lgf; with
+ * either one a zero the index is >= 511, where exp2[511] = 0 or the address
+ * lies past the end of the workgroup's LDS allocation, where gfx950 returns 0
+ * (probed: tools/probes/lds_oob.hip, profiles/r01_lds_oob_probe.log).  So GF
+ * multiply-accumulate needs no zero tests.
+ *
+ * Scaled logs.  The log table holds 128 log v (0xFFFF for zero): 128 is the
+ * stride of the replicated table, so exp(a + b) of scaled logs is the byte at
+ * p + a + b (one v_add3).  Berlekamp-Massey keeps its logs in "address form"
+ * a = 128 log + p (p = this lane's exp byte of entry 0): exp(a) is one
+ * ds_read_u8 at a, exp(a + s) one add; the zero 0xFFFF + p lies past the
+ * allocation end because lgf starts at 96K + 1.
  *
  * Control flow is wave-uniform: loops run to the wave's maximum degree (a
  * ballot-based max over the active lanes) in groups of 4 terms; inside a
@@ -64,15 +71,24 @@
 #define LDS_END (LDS_GF + 512u * GF_REPL * 4u)
 static_assert(LDS_END == 163840u, "lgf must end exactly at the end of the 160 KiB LDS allocation");
 
+typedef __attribute__((address_space(3))) const uint8_t lds_u8;
+
 struct Gf {
-    const uint8_t *p; /* lgf + (lane & 31) * 4 */
-    /* alpha^x for x < 511; 0 for x >= 512 (past the allocation) -- x < 2^24 */
+    const uint8_t *p; /* lgf + (lane & 31) * 4 + 1: this lane's copy of the exp byte of entry 0 */
+    /* alpha^x for x < 511; 0 for x >= 511 (exp2[511] = 0, past it the allocation ends) -- x < 2^24 */
     __device__ __forceinline__ uint32_t exp(uint32_t x) const { return p[x * (GF_REPL * 4)]; }
-    /* log of v < 256 as a register log: ZL for 0 */
-    __device__ __forceinline__ uint32_t log(uint32_t v) const
+    /* scaled log of v < 256: 128 log v, 0xFFFF for v = 0 */
+    __device__ __forceinline__ uint32_t logs(uint32_t v) const
     {
-        return *reinterpret_cast<const uint16_t *>(p + v * (GF_REPL * 4) + 2);
+        return *reinterpret_cast<const uint16_t *>(p + v * (GF_REPL * 4) + 1);
     }
+    /* log of v < 256; 511 for v = 0 (exp of 511 + anything is 0) */
+    __device__ __forceinline__ uint32_t log(uint32_t v) const { return logs(v) >> 7; }
+    /* "address-form" logs (BM): a = 128 log v + (p - LDS base), zero = 0xFFFF + (p - LDS base):
+     * the exp byte of a plus a scaled log s is at LDS byte a + s */
+    __device__ __forceinline__ uint32_t expa(uint32_t a) const { return *(lds_u8 *)(size_t)a; }
+    /* LDS byte address of p (the base of address-form logs) */
+    __device__ __forceinline__ uint32_t pofs() const { return (uint32_t)(size_t)(lds_u8 *)p; }
 };
 
 /* gf_mod of src/internal/common.h:102-110 on the uint16 truncation of v */
@@ -205,36 +221,44 @@ __device__ __forceinline__ bool correct_one(const Gf &gf, const uint4 *__restric
     }
 
     /* ---- Berlekamp-Massey, src/decode.c:49-96 ----
-     * lam: Lambda (poly form) with its logs kept alongside; the logs of
-     * Lambda and of B are packed two per register (u16 halves: entry 2k in
-     * the low half of [k], 2k+1 in the high half; the adds read the halves
-     * through SDWA selects, and B's shift by one entry is one alignbyte per
-     * pair).  dl, db: upper bounds of the nonzero indices of lam and of B;
-     * they only bound the work (zero coefficients contribute zero). */
-#define LLOG(i) (((i) & 1) ? (llp[(i) >> 1] >> 16) : (llp[(i) >> 1] & 0xffffu))
-#define BLOG(i) (((i) & 1) ? (Bp[(i) >> 1] >> 16) : (Bp[(i) >> 1] & 0xffffu))
-    uint32_t llp[RS_NR / 2 + 1], Bp[RS_NR / 2 + 1];
+     * Massey's form of the reference's (Karn's) iteration: B is kept
+     * unnormalised (a copy of an earlier Lambda, shifted) together with the
+     * discrepancy b it was taken at, and the update multiplies by disc / b:
+     *   Lambda += (disc / b) x B,   B <- Lambda (b <- disc) or x B.
+     * Karn's normalised B is B / b, so every product -- and every result --
+     * is the same field element as the reference's.  Lambda lives only in
+     * address-form logs al[] (its coefficients are re-read from exp), B in
+     * bl[] (same form), so the whole state is 2 x 33 VGPRs:
+     *   coefficient update  exp(dq + b_(i-1)) ^ exp(al_i) -> log   (3 lookups)
+     *   discrepancy term    exp(al_i + s_(r-1-i))                  (1 lookup)
+     * dl, db: upper bounds of the nonzero indices of Lambda and of B; they
+     * only bound the work (zero coefficients contribute zero). */
+    const uint32_t pofs = gf.pofs(); /* LDS byte address of this lane's exp(0) */
+    const uint32_t AZ = pofs + 0xFFFFu;                /* address-form zero */
+    uint32_t al[RS_NR + 1], bl[RS_NR + 1];
 #pragma unroll
-    for (int k = 0; k <= RS_NR / 2; ++k) {
-        const uint32_t lo = (uint32_t)(2 * k) <= nemax ? gf.log(lam[2 * k]) : ZL;
-        const uint32_t hi = (2 * k + 1 <= RS_NR && (uint32_t)(2 * k + 1) <= nemax) ? gf.log(lam[2 * k + 1]) : ZL;
-        llp[k] = lo | (hi << 16);
-        Bp[k] = llp[k];
+    for (int i = 0; i <= RS_NR; ++i) {
+        al[i] = (uint32_t)i <= nemax ? gf.logs(lam[i]) + pofs : AZ;
+        bl[i] = al[i];
     }
     uint32_t dl = ne, db = ne, L = ne;
-    /* syndrome window: W entry i (u16 halves, packed like llp) = register
-     * log of S_(r-1-i), ZL where r-1-i < 0; one entry shifts in per
-     * iteration, so the discrepancy terms read it from registers */
+    uint32_t lb = 0; /* scaled log of b (b = 1) */
+    /* syndrome window: W entry i (u16 halves: entry 2k low, 2k+1 high) =
+     * scaled log of S_(r-1-i), 0xFFFF (zero) where r-1-i < 0; one entry
+     * shifts in per iteration, so the discrepancy terms read registers */
     uint32_t W[RS_NR / 2];
 #pragma unroll
     for (int k = 0; k < RS_NR / 2; ++k)
-        W[k] = ZL | (ZL << 16);
+        W[k] = 0xFFFFFFFFu;
     const uint32_t r0 = (ERA ? 63u - wave_max_full(63u - ne) : 0u) + 1u;
     for (uint32_t r = 1; r <= RS_NR; ++r) {
 #pragma unroll
         for (int k = RS_NR / 2 - 1; k > 0; --k)
             W[k] = __builtin_amdgcn_alignbyte(W[k], W[k - 1], 2);
-        W[0] = (W[0] << 16) | conv((uint32_t)srow[(RS_NR - r) * COR_WG]); /* S_(r-1) */
+        {
+            const uint32_t s8 = srow[(RS_NR - r) * COR_WG]; /* S_(r-1), byte log (255 = zero) */
+            W[0] = (W[0] << 16) | (s8 == 255u ? 0xFFFFu : s8 << 7);
+        }
         if (r < r0) /* uniform: before the first codeword's BM step (erasure mode) */
             continue;
         const bool act = r > ne;
@@ -245,43 +269,32 @@ __device__ __forceinline__ bool correct_one(const Gf &gf, const uint4 *__restric
             if ((uint32_t)g <= ub) {
 #pragma unroll
                 for (int i = g; i < g + BM_DISC_G; ++i)
-                    disc ^= gf.exp(LLOG(i) + half(W, i)); /* i >= r: window ZL */
+                    disc ^= gf.expa(al[i] + half(W, i)); /* i >= r: window zero */
             }
         }
-        const uint32_t ld = gf.log(disc);
+        const uint32_t ld = gf.logs(disc);
         const bool upd = act && disc != 0u;
         const bool lengthen = upd && (2u * L <= r + ne - 1u);
-        const bool shift = act && !lengthen;
-        const uint32_t dq = upd ? ld : ZL;   /* Lambda += disc * x * B; zero where nothing is updated */
-        const uint32_t nbias = RS_NN - ld;  /* B = Lambda / disc (lengthen only) */
+        /* scaled log of disc / b; past the allocation where nothing is updated */
+        const int32_t dd = (int32_t)ld - (int32_t)lb;
+        const uint32_t dq = upd ? (uint32_t)(dd < 0 ? dd + 255 * 128 : dd) : (ZL << 7);
         const uint32_t up = min((uint32_t)RS_NR, max(dl, db + 1u));
         const uint32_t ub2 = wave_max_full(act ? up : 0u);
-        /* pairs k = 16..0 (entries 2k+1, 2k), top down: pair k reads the old
-         * pair k-1 (B_(2k-1)) before it is rewritten */
+        /* coefficients top down (index i reads the old bl[i-1] before it is
+         * rewritten); groups of 4 share a uniform bound test */
 #pragma unroll
-        for (int kmax = RS_NR / 2; kmax >= 0; kmax -= BM_UPD_G) {
-            /* groups of 4 pairs (one basic block each, so that their 8 + 8
-             * lookups issue together); pairs past the bound are harmless:
-             * they see zero logs (ZL) and shift zeros */
-            if ((uint32_t)(2 * max(kmax - (BM_UPD_G - 1), 0)) <= ub2) {
+        for (int g = RS_NR; g >= 0; g -= 4) {
+            if ((uint32_t)max(g - 3, 0) <= ub2) {
 #pragma unroll
-                for (int k = kmax; k > kmax - BM_UPD_G && k >= 0; --k) {
-                    const uint32_t blo = k ? BLOG(2 * k - 1) : ZL; /* B_(2k-1): multiplies into lam[2k] */
-                    const uint32_t bhi = BLOG(2 * k);              /* B_(2k): into lam[2k+1] */
-                    const uint32_t nlo = k ? red(LLOG(2 * k) + nbias) : red(nbias); /* lam[0] == 1 */
-                    const uint32_t nhi = red(LLOG(2 * k + 1) + nbias);
-                    const uint32_t bsh = k ? __builtin_amdgcn_alignbyte(Bp[k], Bp[k - 1], 2) : ((Bp[0] << 16) | ZL);
-                    uint32_t lo = LLOG(2 * k), hi = LLOG(2 * k + 1);
-                    if (k) {
-                        lam[2 * k] ^= gf.exp(dq + blo);
-                        lo = gf.log(lam[2 * k]);
+                for (int i = g; i > g - 4 && i >= 0; --i) {
+                    const uint32_t old = al[i];
+                    if (i > 0) {
+                        const uint32_t v = gf.expa(old) ^ gf.expa(dq + bl[i - 1]);
+                        al[i] = gf.logs(v) + pofs;
+                        bl[i] = lengthen ? old : (ERA ? (act ? bl[i - 1] : bl[i]) : bl[i - 1]);
+                    } else {
+                        bl[0] = lengthen ? old : (ERA ? (act ? AZ : bl[0]) : AZ);
                     }
-                    if (2 * k + 1 <= RS_NR) {
-                        lam[2 * k + 1] ^= gf.exp(dq + bhi);
-                        hi = gf.log(lam[2 * k + 1]);
-                    }
-                    Bp[k] = lengthen ? (nlo | (nhi << 16)) : (shift ? bsh : Bp[k]);
-                    llp[k] = lo | (hi << 16);
                 }
             }
         }
@@ -289,16 +302,18 @@ __device__ __forceinline__ bool correct_one(const Gf &gf, const uint4 *__restric
             db = lengthen ? dl : min(db + 1u, (uint32_t)RS_NR);
             if (upd)
                 dl = up;
-            if (lengthen)
+            if (lengthen) {
                 L = r + ne - L;
+                lb = ld;
+            }
         }
     }
     uint32_t ll[RS_NR + 1];
 #pragma unroll
-    for (int i = 0; i <= RS_NR; ++i)
-        ll[i] = LLOG(i);
-#undef LLOG
-#undef BLOG
+    for (int i = 0; i <= RS_NR; ++i) {
+        const uint32_t l = (al[i] - pofs) >> 7;
+        ll[i] = l < 255u ? l : ZL;
+    }
 
     if (P.stop_at == 2u)
         return dl > 40u; /* profiling ablation */
@@ -615,12 +630,13 @@ __global__ __launch_bounds__(COR_WG) void rs_correct_k(const RsDevTables *__rest
     for (uint32_t t = threadIdx.x; t < 512u * GF_REPL; t += COR_WG) {
         const uint32_t x = t / GF_REPL;
         const uint32_t v = x & 255u;
-        lgf[t] = (uint32_t)T->exp2[x] | ((v ? (uint32_t)T->log[v] : ZL) << 16);
+        /* byte 1: exp2[x]; bytes 2-3: scaled log of x & 255 (0xFFFF for 0) */
+        lgf[t] = ((uint32_t)T->exp2[x] << 8) | ((v ? (uint32_t)T->log[v] * 128u : 0xFFFFu) << 16);
     }
     for (uint32_t t = threadIdx.x; t < 16u * 256u; t += COR_WG)
         lch[t] = T->chien[t];
     __syncthreads();
-    const Gf gf{reinterpret_cast<const uint8_t *>(lgf) + (threadIdx.x & (GF_REPL - 1)) * 4};
+    const Gf gf{reinterpret_cast<const uint8_t *>(lgf) + (threadIdx.x & (GF_REPL - 1)) * 4 + 1};
     uint8_t *srow = lsyn + threadIdx.x;
 
     /* The trip count is uniform per workgroup and the whole wave enters the
