@@ -18,6 +18,11 @@
  * through pinned staging in chunks and return when the results are in host
  * memory.  A handle is not reentrant (same rule as the reference handle).
  *
+ * The batch calls serve RS handles and BCH handles (PPLN_FEC_BCH, symbol_size
+ * 3..5): for BCH, `size` is the message byte count (>= the info byte image),
+ * parity rows hold the parity byte image, and there are no erasure or
+ * external-syndrome variants; d_corrected[c] = 0 where d_ok[c] = 0.
+ *
  * Every entry point returns false and records a message (poporon_amd_last_error)
  * on invalid arguments, an unsupported configuration, or a HIP failure.  There
  * is no CPU fallback: without a usable GPU these calls fail.

@@ -333,6 +333,43 @@ class Poporon:
         return ms.value, n.value
 
 
+class Bch(Poporon):
+    """A PPLN_FEC_BCH handle (poporon_bch_config_create + poporon_create): binary
+    BCH over GF(2^m), messages and parity as big-endian byte images
+    (src/encode.c:199-233, src/decode.c:542-590).  Same methods as
+    :class:`Poporon`; ``parity_size``/``info_size`` are the byte-image sizes."""
+
+    def __init__(self, symbol_size=4, generator_polynomial=0x13, correction_capability=3, device=None):
+        self.lib = load_library()
+        self.erasure = None
+        self._syn = None
+        cfg = self.lib.poporon_bch_config_create(symbol_size, generator_polynomial, correction_capability)
+        if not cfg:
+            raise PoporonError("poporon_bch_config_create returned NULL")
+        self.h = self.lib.poporon_create(cfg)
+        self.lib.poporon_config_destroy(cfg)
+        if not self.h:
+            raise PoporonError(f"poporon_create returned NULL {last_error()}")
+        self.num_roots = int(self.lib.poporon_get_parity_size(self.h))  # parity bytes (array shapes)
+        if device is not None:
+            self._check(self.lib.poporon_amd_set_device(self.h, device), "poporon_amd_set_device")
+
+    @classmethod
+    def default(cls, **kw):
+        """poporon_config_bch_default(): BCH(15, 5) over GF(16), 0x13, t = 3."""
+        return cls(4, 0x13, 3, **kw)
+
+    def decode(self, data, parity, corrected_init=0):
+        """poporon_decode on copies: (ok, corrected_num, data').  As in the
+        reference, corrected_num is left at corrected_init on failure."""
+        d = _u8(data, copy=True)
+        p = _u8(parity, copy=True)
+        n = C.c_size_t(corrected_init)
+        ok = self.lib.poporon_decode(self.h, _buf(d) if d.size else _buf(np.zeros(1, np.uint8)), d.size,
+                                     _buf(p) if p.size else _buf(np.zeros(1, np.uint8)), C.byref(n))
+        return bool(ok), int(n.value), d
+
+
 def channel_xor_device(d_positions, d_magnitudes, per_codeword, d_codewords, stride, count, stream=0):
     """Test/benchmark channel: XOR magnitudes into positions of each codeword row (device pointers, async)."""
     if not load_library().poporon_amd_channel_xor_device(d_positions, d_magnitudes, per_codeword, d_codewords,

@@ -30,6 +30,7 @@
 #include "poporon_amd.h"
 #include "rs_device.h"
 #include "rs_generic.h"
+#include "bch_device.h"
 
 #ifndef POPORON_BUILDTIME
 #define POPORON_BUILDTIME 1
@@ -101,6 +102,7 @@ struct _poporon_config_t {
     uint8_t num_roots;
     poporon_erasure_t *erasure;
     uint16_t *syndrome;
+    uint8_t correction_capability; /* BCH */
 };
 
 #define NKERN 4
@@ -153,6 +155,10 @@ struct _poporon_t {
     RsCorrParams corr;
     RsGenTables gen_tab;
     RsGenParams gen;
+    /* PPLN_FEC_BCH handles (rs == nullptr) */
+    poporon_gf_t *bgf;
+    BchParams bch;
+    bool bch_ok; /* codewords fit 31 bits: served by bch.hip */
     GpuCtx gpu;
 };
 
@@ -361,8 +367,8 @@ EXPORT poporon_config_t *poporon_config_rs_default(void)
     return poporon_rs_config_create(8, 0x11D, 1, 1, 32, nullptr, nullptr);
 }
 
-/* LDPC and BCH are outside this build's scope:
- * exported so that callers link, but they construct nothing. */
+/* LDPC is outside this build's scope: exported
+ * so that callers link, but it constructs nothing. */
 EXPORT poporon_config_t *poporon_ldpc_config_create(size_t, poporon_ldpc_rate_t, poporon_ldpc_matrix_type_t, uint32_t,
                                                     bool, bool, bool, uint32_t, uint32_t, uint32_t, const int8_t *,
                                                     size_t, uint64_t)
@@ -370,10 +376,17 @@ EXPORT poporon_config_t *poporon_ldpc_config_create(size_t, poporon_ldpc_rate_t,
     fail("LDPC is not provided by libpoporon_amd");
     return nullptr;
 }
-EXPORT poporon_config_t *poporon_bch_config_create(uint8_t, uint16_t, uint8_t)
+EXPORT poporon_config_t *poporon_bch_config_create(uint8_t symbol_size, uint16_t generator_polynomial,
+                                                   uint8_t correction_capability)
 {
-    fail("BCH is not provided by libpoporon_amd");
-    return nullptr;
+    poporon_config_t *c = (poporon_config_t *)calloc(1, sizeof(poporon_config_t));
+    if (!c)
+        return nullptr;
+    c->fec_type = PPLN_FEC_BCH;
+    c->symbol_size = symbol_size;
+    c->generator_polynomial = generator_polynomial;
+    c->correction_capability = correction_capability;
+    return c;
 }
 EXPORT poporon_config_t *poporon_config_ldpc_default(size_t, poporon_ldpc_rate_t)
 {
@@ -385,11 +398,7 @@ EXPORT poporon_config_t *poporon_config_ldpc_burst_resistant(size_t, poporon_ldp
     fail("LDPC is not provided by libpoporon_amd");
     return nullptr;
 }
-EXPORT poporon_config_t *poporon_config_bch_default(void)
-{
-    fail("BCH is not provided by libpoporon_amd");
-    return nullptr;
-}
+EXPORT poporon_config_t *poporon_config_bch_default(void) { return poporon_bch_config_create(4, 0x13, 3); }
 
 EXPORT void poporon_config_destroy(poporon_config_t *config) { free(config); }
 
@@ -520,12 +529,95 @@ static bool params_supported(const poporon_t *h)
     return true;
 }
 
+/* ---- BCH handle: generator from minimal polynomials (src/bch.c:184-285) ---- */
+static uint32_t bch_min_poly(const poporon_gf_t *gf, uint32_t e)
+{
+    uint16_t p[64];
+    uint32_t deg = 0, c = e, out = 0;
+    memset(p, 0, sizeof(p));
+    p[0] = 1;
+    do {
+        const uint16_t root = gf->log2exp[c];
+        for (int j = (int)deg; j >= 0; j--) {
+            if (j + 1 < 64)
+                p[j + 1] ^= p[j];
+            p[j] = (p[j] && root) ? gf->log2exp[(gf->exp2log[p[j]] + gf->exp2log[root]) % gf->field_size] : 0;
+        }
+        deg++;
+        c = (c * 2) % gf->field_size;
+    } while (c != e);
+    for (uint32_t i = 0; i <= deg && i < 32; i++)
+        if (p[i] == 1)
+            out |= 1u << i;
+    return out;
+}
+
+static poporon_t *create_bch(const poporon_config_t *config)
+{
+    const uint32_t m = config->symbol_size, t = config->correction_capability;
+    if (m < 3 || m > 16 || t < 1 || t > 16) /* src/bch.c:290-296 */
+        return nullptr;
+    poporon_gf_t *gf = poporon_gf_create(config->symbol_size, config->generator_polynomial);
+    if (!gf)
+        return nullptr;
+    poporon_t *h = new (std::nothrow) _poporon_t();
+    if (!h) {
+        poporon_gf_destroy(gf);
+        return nullptr;
+    }
+    h->fec_type = PPLN_FEC_BCH;
+    h->rs = nullptr;
+    h->bgf = gf;
+    BchParams &b = h->bch;
+    memset(&b, 0, sizeof(b));
+    b.m = m;
+    b.nn = gf->field_size;
+    b.t = t;
+    /* codewords of more than 31 bits overflow the reference's uint32 shifts
+     * (undefined behaviour): the handle exists, its codec calls fail */
+    h->bch_ok = m <= 5;
+    if (h->bch_ok) {
+        std::vector<uint8_t> used(b.nn + 1, 0);
+        uint32_t gen = 1, gdeg = 0;
+        for (uint32_t i = 1; i <= 2 * t; i++) {
+            const uint32_t e = i % b.nn;
+            if (used[e])
+                continue;
+            uint32_t c = e;
+            do {
+                used[c] = 1;
+                c = (c * 2) % b.nn;
+            } while (c != e);
+            const uint32_t mp = bch_min_poly(gf, e);
+            uint32_t prod = 0;
+            for (uint32_t j = 0; j <= gdeg; j++)
+                if (gen & (1u << j))
+                    prod ^= mp << j;
+            gen = prod;
+            gdeg = 31u - (uint32_t)__builtin_clz(gen);
+        }
+        b.gen = gen;
+        b.gdeg = gdeg;
+        b.pbits = gdeg;
+        b.k = b.nn - gdeg;
+        b.dbytes = (b.k + 7) / 8;
+        b.pbytes = (b.pbits + 7) / 8;
+        for (uint32_t i = 0; i < 32; i++) {
+            b.alog[i] = i <= b.nn ? (uint8_t)gf->log2exp[i] : 0;
+            b.log[i] = i <= b.nn ? (uint8_t)gf->exp2log[i] : 0;
+        }
+    }
+    return h;
+}
+
 EXPORT poporon_t *poporon_create(const poporon_config_t *config)
 {
     if (!config)
         return nullptr;
+    if (config->fec_type == PPLN_FEC_BCH)
+        return create_bch(config);
     if (config->fec_type != PPLN_FEC_RS) {
-        fail("only PPLN_FEC_RS is provided by libpoporon_amd");
+        fail("LDPC is not provided by libpoporon_amd");
         return nullptr;
     }
     poporon_rs_t *rs = poporon_rs_create(config->symbol_size, config->generator_polynomial,
@@ -608,15 +700,28 @@ EXPORT void poporon_destroy(poporon_t *h)
         return;
     gpu_release(h->gpu);
     poporon_rs_destroy(h->rs);
+    poporon_gf_destroy(h->bgf);
     delete h;
 }
 
 EXPORT poporon_fec_type_t poporon_get_fec_type(const poporon_t *h) { return h ? h->fec_type : PPLN_FEC_UNKNOWN; }
 EXPORT uint32_t poporon_get_iterations_used(const poporon_t *) { return 0; }
-EXPORT size_t poporon_get_parity_size(const poporon_t *h) { return h ? h->rs->num_roots : 0; }
+/* src/poporon.c:322-362: BCH sizes are the byte images of the parity / data bits */
+EXPORT size_t poporon_get_parity_size(const poporon_t *h)
+{
+    if (!h)
+        return 0;
+    if (h->fec_type == PPLN_FEC_BCH)
+        return h->bch_ok ? h->bch.pbytes : 0;
+    return h->rs->num_roots;
+}
 EXPORT size_t poporon_get_info_size(const poporon_t *h)
 {
-    return h ? (size_t)(h->rs->gf->field_size - h->rs->num_roots) : 0;
+    if (!h)
+        return 0;
+    if (h->fec_type == PPLN_FEC_BCH)
+        return h->bch_ok ? h->bch.dbytes : 0;
+    return (size_t)(h->rs->gf->field_size - h->rs->num_roots);
 }
 EXPORT uint32_t poporon_version_id(void) { return (uint32_t)POPORON_VERSION_ID; }
 EXPORT poporon_buildtime_t poporon_buildtime(void) { return (poporon_buildtime_t)POPORON_BUILDTIME; }
@@ -670,7 +775,9 @@ static bool gpu_init(poporon_t *h)
     GpuCtx &g = h->gpu;
     if (g.ready)
         return true;
-    if (!h->supported)
+    if (h->fec_type == PPLN_FEC_BCH && !h->bch_ok)
+        return fail("BCH codewords longer than 31 bits (symbol_size > 5) are not served");
+    if (h->fec_type == PPLN_FEC_RS && !h->supported)
         return fail("RS parameters not served by the GPU kernels (need 2 <= symbol_size <= 8 and "
                     "1 <= num_roots < 2^symbol_size - 1)");
     int n = 0;
@@ -690,7 +797,9 @@ static bool gpu_init(poporon_t *h)
     HIP_OK(hipGetDeviceProperties(&prop, g.device));
     g.num_cu = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
     HIP_OK(hipStreamCreateWithFlags(&g.stream, hipStreamNonBlocking));
-    if (h->fast) {
+    if (h->fec_type == PPLN_FEC_BCH) {
+        /* parameters and tables go by value with every launch */
+    } else if (h->fast) {
         HIP_OK(hipMalloc((void **)&g.tab, sizeof(RsDevTables)));
         HIP_OK(hipMemcpy(g.tab, &h->host_tab, sizeof(RsDevTables), hipMemcpyHostToDevice));
     } else {
@@ -745,11 +854,24 @@ EXPORT bool poporon_amd_reserve(poporon_t *h, size_t max_count)
     return ensure_rem(h, max_count);
 }
 
+/* parity bytes per codeword: num_roots (RS) or the BCH parity byte image */
+static size_t par_bytes(const poporon_t *h)
+{
+    return h->fec_type == PPLN_FEC_BCH ? h->bch.pbytes : h->rs->num_roots;
+}
+
+/* largest decodable message size (RS: src/decode.c:418-429); BCH: no upper bound */
+static size_t kmax(const poporon_t *h)
+{
+    return h->fec_type == PPLN_FEC_BCH ? (size_t)-1 : (size_t)h->rs->gf->field_size - h->rs->num_roots;
+}
+
 static bool check_decode_size(const poporon_t *h, size_t size)
 {
+    if (h->fec_type == PPLN_FEC_BCH) /* src/decode.c:553-555, :598 */
+        return size >= 1 && size >= h->bch.dbytes;
     /* src/decode.c:418-429: pad = nn - nroots - size must lie in [0, nn - nroots) */
-    const size_t kmax = (size_t)h->rs->gf->field_size - h->rs->num_roots;
-    return size >= 1 && size <= kmax;
+    return size >= 1 && size <= kmax(h);
 }
 
 /* ------------------------------------------------------------------------ */
@@ -848,7 +970,9 @@ static bool launch_encode(poporon_t *h, const uint8_t *d_data, size_t ds, uint8_
                           size_t count, hipStream_t s)
 {
     KernelTimer t(h->gpu, POPORON_AMD_KERNEL_ENCODE, s);
-    if (h->fast) {
+    if (h->fec_type == PPLN_FEC_BCH) {
+        HIP_OK(bchk_encode(&h->bch, d_data, ds, d_par, ps, count, h->gpu.num_cu, s));
+    } else if (h->fast) {
         HIP_OK(rsk_encode(h->gpu.tab, d_data, ds, d_par, ps, (uint32_t)size, count, h->gpu.num_cu, s));
     } else {
         RsGenParams prm = h->gen;
@@ -864,6 +988,14 @@ static bool launch_decode(poporon_t *h, uint8_t *d_data, size_t ds, uint8_t *d_p
                           const uint32_t *pos32, size_t pos_stride, const uint8_t *cnt, uint8_t *ok,
                           uint8_t *corrected, hipStream_t s, uint8_t *rem = nullptr)
 {
+    if (h->fec_type == PPLN_FEC_BCH) {
+        if (ext_syn || pos8 || pos32)
+            return fail("BCH has no erasure or external-syndrome decode");
+        KernelTimer t(h->gpu, POPORON_AMD_KERNEL_CORRECT, s);
+        HIP_OK(bchk_decode(&h->bch, d_data, ds, d_par, ps, count, ok, corrected, h->gpu.num_cu, s));
+        t.done();
+        return true;
+    }
     if (!h->fast) {
         RsGenParams prm = h->gen;
         prm.size = (uint32_t)size;
@@ -900,8 +1032,10 @@ EXPORT bool poporon_check_batch_device(poporon_t *h, const uint8_t *d_data, size
 {
     if (!h || (count && (!d_data || !d_parity || !d_dirty)))
         return fail("NULL argument");
+    if (h->fec_type != PPLN_FEC_RS)
+        return fail("poporon_check_batch_device serves RS handles");
     if (!check_decode_size(h, size))
-        return fail("size %zu outside [1, %u]", size, (unsigned)(h->rs->gf->field_size - h->rs->num_roots));
+        return fail("size %zu outside [1, %u]", size, (unsigned)kmax(h));
     if (!gpu_init(h))
         return false;
     DeviceGuard dg(h->gpu.device);
@@ -940,10 +1074,10 @@ EXPORT bool poporon_decode_batch_device(poporon_t *h, uint8_t *d_data, size_t da
 {
     if (!h || (count && (!d_data || !d_parity || !d_ok)))
         return fail("NULL argument");
-    if (d_positions && (!d_counts || positions_stride < h->rs->num_roots))
-        return fail("erasure batch needs counts and positions_stride >= num_roots (%u)", (unsigned)h->rs->num_roots);
+    if (d_positions && (h->fec_type != PPLN_FEC_RS || !d_counts || positions_stride < h->rs->num_roots))
+        return fail("erasure batch needs an RS handle, counts and positions_stride >= num_roots");
     if (!check_decode_size(h, size))
-        return fail("decode size %zu outside [1, %u]", size, (unsigned)(h->rs->gf->field_size - h->rs->num_roots));
+        return fail("decode size %zu outside [1, %u]", size, (unsigned)kmax(h));
     if (!gpu_init(h))
         return false;
     DeviceGuard dg(h->gpu.device);
@@ -958,10 +1092,12 @@ EXPORT bool poporon_decode_batch_syndrome_device(poporon_t *h, uint8_t *d_data, 
 {
     if (!h || (count && (!d_data || !d_parity || !d_ok || !d_syndromes)))
         return fail("NULL argument");
+    if (h->fec_type != PPLN_FEC_RS)
+        return fail("external-syndrome decode serves RS handles");
     if (syndrome_stride < h->rs->num_roots)
         return fail("syndrome_stride < num_roots (%u)", (unsigned)h->rs->num_roots);
     if (!check_decode_size(h, size))
-        return fail("decode size %zu outside [1, %u]", size, (unsigned)(h->rs->gf->field_size - h->rs->num_roots));
+        return fail("decode size %zu outside [1, %u]", size, (unsigned)kmax(h));
     if (!gpu_init(h))
         return false;
     DeviceGuard dg(h->gpu.device);
@@ -1056,7 +1192,7 @@ EXPORT bool poporon_encode_batch(poporon_t *h, const uint8_t *data, size_t data_
         return false;
     DeviceGuard dg(h->gpu.device);
     GpuCtx &g = h->gpu;
-    const size_t nr = h->rs->num_roots;
+    const size_t nr = par_bytes(h);
     const size_t chunk = std::max<size_t>(1, std::min(count, kPipeChunk));
     for (auto &ps : g.pipe)
         if (!pipe_slot(h, ps, chunk * (size + nr) + 64))
@@ -1103,15 +1239,15 @@ EXPORT bool poporon_decode_batch(poporon_t *h, uint8_t *data, size_t data_stride
 {
     if (!h || (count && (!data || !parity || !ok)))
         return fail("NULL argument");
-    if (positions && (!counts || positions_stride < h->rs->num_roots))
-        return fail("erasure batch needs counts and positions_stride >= num_roots (%u)", (unsigned)h->rs->num_roots);
+    if (positions && (h->fec_type != PPLN_FEC_RS || !counts || positions_stride < h->rs->num_roots))
+        return fail("erasure batch needs an RS handle, counts and positions_stride >= num_roots");
     if (!check_decode_size(h, size))
-        return fail("decode size %zu outside [1, %u]", size, (unsigned)(h->rs->gf->field_size - h->rs->num_roots));
+        return fail("decode size %zu outside [1, %u]", size, (unsigned)kmax(h));
     if (!gpu_init(h))
         return false;
     DeviceGuard dg(h->gpu.device);
     GpuCtx &g = h->gpu;
-    const size_t nr = h->rs->num_roots;
+    const size_t nr = par_bytes(h);
     const size_t w = size + nr;
     const size_t chunk = std::max<size_t>(1, std::min(count, kPipeChunk));
     /* slot layout: [codewords w*n | ok n | cor n | positions nr*n | counts n | syndrome workspace 32*n (device)] */
@@ -1189,7 +1325,9 @@ EXPORT bool poporon_encode(poporon_t *h, uint8_t *data, size_t size, uint8_t *pa
 {
     if (!h || !data || !parity)
         return false;
-    if (h->fec_type != PPLN_FEC_RS)
+    if (h->fec_type == PPLN_FEC_BCH && size < h->bch.dbytes) /* src/encode.c:210-212 */
+        return false;
+    if (h->fec_type != PPLN_FEC_RS && h->fec_type != PPLN_FEC_BCH)
         return false;
     if (size > 65535) /* the reference's uint16 counter loops forever here (quirk Q7) */
         return fail("size %zu > 65535", size);
@@ -1197,7 +1335,7 @@ EXPORT bool poporon_encode(poporon_t *h, uint8_t *data, size_t size, uint8_t *pa
         return false;
     DeviceGuard dg(h->gpu.device);
     GpuCtx &g = h->gpu;
-    const size_t nr = h->rs->num_roots;
+    const size_t nr = par_bytes(h);
     if (!ensure_stage(h, size + nr + 16))
         return false;
     uint8_t *dd = g.stage, *dp = g.stage + ((size + 15) & ~(size_t)15);
@@ -1210,10 +1348,45 @@ EXPORT bool poporon_encode(poporon_t *h, uint8_t *data, size_t size, uint8_t *pa
     return true;
 }
 
+/* src/decode.c:542-590: data bytes and corrected_num are written on success only */
+static bool bch_decode_one(poporon_t *h, uint8_t *data, size_t size, uint8_t *parity, size_t *corrected_num)
+{
+    if (size < h->bch.dbytes)
+        return false;
+    if (!gpu_init(h))
+        return false;
+    DeviceGuard dg(h->gpu.device);
+    GpuCtx &g = h->gpu;
+    const size_t db = h->bch.dbytes, pb = h->bch.pbytes;
+    if (!ensure_stage(h, db + pb + 2 + 16))
+        return false;
+    uint8_t *dd = g.stage, *dp = g.stage + db, *dok = dp + pb;
+    if (db)
+        HIP_OK(hipMemcpyAsync(dd, data, db, hipMemcpyHostToDevice, g.stream));
+    if (pb)
+        HIP_OK(hipMemcpyAsync(dp, parity, pb, hipMemcpyHostToDevice, g.stream));
+    if (!launch_decode(h, dd, db, dp, pb, db, 1, nullptr, 0, nullptr, nullptr, 0, nullptr, dok, dok + 1, g.stream))
+        return false;
+    uint8_t res[2];
+    uint8_t out[4];
+    HIP_OK(hipMemcpyAsync(res, dok, 2, hipMemcpyDeviceToHost, g.stream));
+    if (db)
+        HIP_OK(hipMemcpyAsync(out, dd, db, hipMemcpyDeviceToHost, g.stream));
+    HIP_OK(hipStreamSynchronize(g.stream));
+    if (!res[0])
+        return false;
+    memcpy(data, out, db);
+    if (corrected_num)
+        *corrected_num = res[1];
+    return true;
+}
+
 EXPORT bool poporon_decode(poporon_t *h, uint8_t *data, size_t size, uint8_t *parity, size_t *corrected_num)
 {
     if (!h || !data || !parity || !size)
         return false;
+    if (h->fec_type == PPLN_FEC_BCH)
+        return bch_decode_one(h, data, size, parity, corrected_num);
     if (h->fec_type != PPLN_FEC_RS)
         return false;
     size_t fixed = 0;

@@ -261,3 +261,90 @@ class Reference:
         log = np.array([gf.exp2log[i] for i in range(nn + 1)], np.uint16)
         gen = np.array([rs.generator_polynomial[i] for i in range(rs.num_roots + 1)], np.uint16)
         return alog, log, gen, h.buffer.contents.primitive_inverse
+
+
+# -----------------------------------------------------------------------------
+# binary BCH (oracle/bch_oracle.c) and the reference's BCH handle
+# -----------------------------------------------------------------------------
+class BchOracle:
+    """Clean-room restatement of the reference's BCH codec (oracle/bch_oracle.c)."""
+
+    def __init__(self, m=4, poly=0x13, t=3, so=ORACLE_SO):
+        L = self.lib = C.CDLL(so)
+        L.oracle_bch_sizeof.restype = C.c_size_t
+        L.oracle_bch_init.argtypes = [C.c_void_p, C.c_uint8, C.c_uint16, C.c_uint8]
+        L.oracle_bch_data_bits.argtypes = L.oracle_bch_parity_bits.argtypes = [C.c_void_p]
+        L.oracle_bch_data_bits.restype = L.oracle_bch_parity_bits.restype = C.c_uint32
+        L.oracle_bch_encode.argtypes = [C.c_void_p, _u8p, C.c_size_t, _u8p]
+        L.oracle_bch_decode.argtypes = [C.c_void_p, _u8p, C.c_size_t, _u8p, C.POINTER(C.c_size_t)]
+        self._buf = C.create_string_buffer(L.oracle_bch_sizeof())
+        self.h = C.cast(self._buf, C.c_void_p)
+        rc = L.oracle_bch_init(self.h, m, poly, t)
+        if rc != 0:
+            raise ValueError(f"oracle_bch_init: {rc}")
+        self.k = L.oracle_bch_data_bits(self.h)
+        self.pbits = L.oracle_bch_parity_bits(self.h)
+        self.data_bytes = (self.k + 7) // 8
+        self.parity_bytes = (self.pbits + 7) // 8
+
+    def encode(self, data):
+        d = np.ascontiguousarray(data, dtype=np.uint8)
+        par = np.zeros(max(1, self.parity_bytes), np.uint8)
+        ok = self.lib.oracle_bch_encode(self.h, _ptr(d) if d.size else _ptr(np.zeros(1, np.uint8)), d.size,
+                                        _ptr(par))
+        return bool(ok), par[: self.parity_bytes]
+
+    def decode(self, data, parity, corrected_init=0):
+        d = np.array(data, dtype=np.uint8, copy=True)
+        p = np.ascontiguousarray(parity, dtype=np.uint8)
+        n = C.c_size_t(corrected_init)
+        ok = self.lib.oracle_bch_decode(self.h, _ptr(d) if d.size else _ptr(np.zeros(1, np.uint8)), d.size,
+                                        _ptr(p) if p.size else _ptr(np.zeros(1, np.uint8)), C.byref(n))
+        return bool(ok), int(n.value), d
+
+
+class ReferenceBch:
+    """libpoporon's BCH handle (oracle/_ref), driven through poporon_encode/decode."""
+
+    def __init__(self, m=4, poly=0x13, t=3, so=REF_SO):
+        L = self.lib = C.CDLL(so)
+        L.poporon_bch_config_create.restype = C.c_void_p
+        L.poporon_bch_config_create.argtypes = [C.c_uint8, C.c_uint16, C.c_uint8]
+        L.poporon_create.restype = C.c_void_p
+        L.poporon_create.argtypes = [C.c_void_p]
+        L.poporon_destroy.argtypes = [C.c_void_p]
+        L.poporon_config_destroy.argtypes = [C.c_void_p]
+        L.poporon_encode.argtypes = [C.c_void_p, _u8p, C.c_size_t, _u8p]
+        L.poporon_encode.restype = C.c_bool
+        L.poporon_decode.argtypes = [C.c_void_p, _u8p, C.c_size_t, _u8p, C.POINTER(C.c_size_t)]
+        L.poporon_decode.restype = C.c_bool
+        L.poporon_get_parity_size.argtypes = L.poporon_get_info_size.argtypes = [C.c_void_p]
+        L.poporon_get_parity_size.restype = L.poporon_get_info_size.restype = C.c_size_t
+        cfg = L.poporon_bch_config_create(m, poly, t)
+        self.h = L.poporon_create(cfg)
+        L.poporon_config_destroy(cfg)
+        if not self.h:
+            raise ValueError("poporon_create returned NULL")
+        self.parity_bytes = L.poporon_get_parity_size(self.h)
+        self.info_bytes = L.poporon_get_info_size(self.h)
+
+    def close(self):
+        if self.h:
+            self.lib.poporon_destroy(self.h)
+            self.h = None
+
+    __del__ = close
+
+    def encode(self, data):
+        d = np.array(data, dtype=np.uint8, copy=True)
+        par = np.zeros(max(1, self.parity_bytes), np.uint8)
+        ok = self.lib.poporon_encode(self.h, _ptr(d) if d.size else _ptr(np.zeros(1, np.uint8)), d.size, _ptr(par))
+        return bool(ok), par[: self.parity_bytes]
+
+    def decode(self, data, parity, corrected_init=0):
+        d = np.array(data, dtype=np.uint8, copy=True)
+        p = np.array(parity, dtype=np.uint8, copy=True)
+        n = C.c_size_t(corrected_init)
+        ok = self.lib.poporon_decode(self.h, _ptr(d) if d.size else _ptr(np.zeros(1, np.uint8)), d.size,
+                                     _ptr(p) if p.size else _ptr(np.zeros(1, np.uint8)), C.byref(n))
+        return bool(ok), int(n.value), d

@@ -51,9 +51,11 @@ def test_invalid_handles(lib):
 
 
 def test_out_of_scope_codecs_return_null(lib):
-    assert not lib.poporon_config_bch_default()
     assert not lib.poporon_config_ldpc_default(64, 1)
-    assert not lib.poporon_bch_config_create(4, 0x13, 3)
+    assert not lib.poporon_config_ldpc_burst_resistant(64, 1)
+    cfg = lib.poporon_config_bch_default()  # BCH is served (bch.hip)
+    assert cfg
+    lib.poporon_config_destroy(cfg)
 
 
 def test_rs_handle_getters():
@@ -162,3 +164,23 @@ def test_gf_mod_is_uint16_modulo():
         magic = (1 << 32) // nn + 1
         q = (v * magic) >> 32
         assert (v - q * nn == v % nn).all(), m
+
+
+def test_bch_handles_and_getters():
+    """BCH handles (src/poporon.c:148-170, :265-298): getters are the byte-image
+    sizes of the reference (tests/golden/bch_golden.npz), invalid parameters give NULL."""
+    import os
+    g = np.load(os.path.join(os.path.dirname(__file__), "golden", "bch_golden.npz"))
+    for gi, (m, poly, t) in enumerate(g["params"]):
+        h = P.Bch(int(m), int(poly), int(t))
+        assert h.fec_type == P.POPORON_FEC_BCH
+        assert (h.parity_size, h.info_size) == tuple(int(x) for x in g[f"b{gi}_sizes"])
+        assert h.lib.poporon_get_iterations_used(h.h) == 0
+    d = P.Bch.default()
+    assert (d.parity_size, d.info_size) == (2, 1)
+    for bad in ((2, 0x7, 1), (17, 0x11D, 1), (4, 0x13, 0), (4, 0x13, 17), (4, 0x11, 2)):
+        with pytest.raises(P.PoporonError):
+            P.Bch(*bad)
+    big = P.Bch(6, 0x43, 2)  # 63-bit codewords: created (as the reference), codec refused
+    with pytest.raises(P.PoporonError, match="31 bits"):
+        big.encode(np.zeros(8, np.uint8))

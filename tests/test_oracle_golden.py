@@ -169,3 +169,44 @@ def test_oracle_general_parameters_golden(pgolden, gi):
     for syn, inp, out, ok, cor in zip(g("xs_syn"), g("xs_in"), g("xs_out"), g("xs_ok"), g("xs_cor")):
         gok, gn, gd, gp = o.decode(inp[:k], inp[k:k + nr], ext_syn=syn)
         assert gok == bool(ok) and gn == cor and (np.concatenate([gd, gp]) == out[:k + nr]).all()
+
+
+# ---------------------------------------------------------------------------
+# binary BCH (tests/golden/bch_golden.npz, tools/gen_golden_bch.py)
+# ---------------------------------------------------------------------------
+@pytest.fixture(scope="module")
+def bgolden():
+    import os
+    return np.load(os.path.join(os.path.dirname(__file__), "golden", "bch_golden.npz"))
+
+
+@pytest.mark.parametrize("gi", range(12))
+def test_bch_oracle_golden(bgolden, gi):
+    from oracle import BchOracle
+    m, poly, t = (int(x) for x in bgolden["params"][gi])
+    o = BchOracle(m, poly, t)
+    g = lambda k: bgolden[f"b{gi}_{k}"]  # noqa: E731
+    pb, ib = (int(x) for x in g("sizes"))
+    assert (o.parity_bytes, o.data_bytes) == (pb, ib)
+    for d, p in zip(g("enc_data"), g("enc_parity")):
+        ok, par = o.encode(d[:ib])
+        assert ok and (par == p[:pb]).all()
+    for d, p, out, ok, cor in zip(g("dec_data"), g("dec_parity"), g("dec_out"), g("dec_ok"), g("dec_cor")):
+        gok, gn, gd = o.decode(d[:ib], p[:pb], 777)  # 777: left untouched on failure, as the reference
+        assert gok == bool(ok) and gn == cor and (gd == out[:ib]).all()
+
+
+def test_bch_oracle_vs_reference_random():
+    if not reference_available():
+        pytest.skip("oracle/_ref not built")
+    from oracle import BchOracle, ReferenceBch
+    rng = np.random.default_rng(5)
+    for m, poly, t in ((4, 0x13, 3), (5, 0x25, 3), (5, 0x25, 6), (3, 0x0B, 1)):
+        o, r = BchOracle(m, poly, t), ReferenceBch(m, poly, t)
+        ib, pb = o.data_bytes, o.parity_bytes
+        for _ in range(3000):
+            d = rng.integers(0, 256, ib, dtype=np.uint8)
+            p = rng.integers(0, 256, pb, dtype=np.uint8)
+            assert (o.encode(d)[1] == r.encode(d)[1]).all()
+            a, b = o.decode(d, p, 5), r.decode(d, p, 5)
+            assert a[0] == b[0] and a[1] == b[1] and (a[2] == b[2]).all()
