@@ -3,21 +3,22 @@
  *
  * Same symbols, signatures, enums and macros as the reference's
  * include/poporon.h:22-99 (libpoporon, colopl/libpoporon), so existing
- * callers recompile and relink unchanged.  The Reed-Solomon codec is served
- * by HIP kernels; LDPC and BCH are outside this build's scope: their config
+ * callers recompile and relink unchanged.  The Reed-Solomon and BCH codecs
+ * are served by HIP kernels; LDPC is outside this build's scope: its config
  * constructors are exported so callers still link, but return NULL.
  *
  *   reference symbol                     replaced by (this header)
  *   poporon_rs_config_create    poporon.h:67-69   -> same, src/api.cpp
  *   poporon_ldpc_config_create  poporon.h:71-76   -> stub, returns NULL
- *   poporon_bch_config_create   poporon.h:78-79   -> stub, returns NULL
+ *   poporon_bch_config_create   poporon.h:78-79   -> same (BCH kernels, symbol_size 3..5)
  *   poporon_config_rs_default   poporon.h:81      -> same (8, 0x11D, 1, 1, 32)
- *   poporon_config_ldpc_default / _burst_resistant / poporon_config_bch_default
- *                               poporon.h:82-84   -> stubs, return NULL
+ *   poporon_config_ldpc_default / _burst_resistant
+ *                               poporon.h:82-83   -> stubs, return NULL
+ *   poporon_config_bch_default  poporon.h:84      -> same (4, 0x13, 3)
  *   poporon_config_destroy      poporon.h:85
  *   poporon_create / _destroy   poporon.h:87-88
- *   poporon_encode              poporon.h:90      -> RS encode kernel (batch of one)
- *   poporon_decode              poporon.h:91      -> RS syndrome + correction kernels
+ *   poporon_encode              poporon.h:90      -> RS / BCH encode kernel (batch of one)
+ *   poporon_decode              poporon.h:91      -> RS syndrome + correction / BCH decode kernels
  *   poporon_get_fec_type / _iterations_used / _parity_size / _info_size
  *                               poporon.h:93-96
  *   poporon_version_id / poporon_buildtime
@@ -35,6 +36,7 @@
 
 #include "poporon/erasure.h"
 #include "poporon/gf.h"
+#include "poporon/rng.h"
 
 #define POPORON_FEC_RS      1
 #define POPORON_FEC_LDPC    2

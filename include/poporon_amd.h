@@ -123,6 +123,13 @@ bool poporon_decode_batch(poporon_t *pprn, uint8_t *data, size_t data_stride, ui
 bool poporon_amd_timing(poporon_t *pprn, int enable);
 bool poporon_amd_timing_read(poporon_t *pprn, int kernel, double *total_ms, uint64_t *launches);
 
+/* ---- deterministic payloads -------------------------------------------------
+ * Write size bytes of rng's stream (the bytes poporon_rng_next(rng, dest, size)
+ * would write, include/poporon/rng.h) into device memory d_dest, on stream
+ * (the current HIP device), and advance rng as that call would.  The block
+ * start states are derived on the host by GF(2) jump-ahead (rng.hip). */
+bool poporon_amd_rng_fill_device(poporon_rng_t *rng, void *d_dest, size_t size, void *stream);
+
 /* ---- test / benchmark utility (not part of the codec) ---------------------
  * Symbol-error channel: for each of count codeword rows (stride bytes apart)
  * XOR d_magnitudes[c*per_codeword + e] into byte d_positions[c*per_codeword + e]

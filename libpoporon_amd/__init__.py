@@ -84,6 +84,10 @@ _SIGS = {
     "poporon_encode_batch": (C.c_bool, [_vp, _vp, C.c_size_t, _vp, C.c_size_t, C.c_size_t, C.c_size_t]),
     "poporon_decode_batch": (C.c_bool, [_vp, _vp, C.c_size_t, _vp, C.c_size_t, C.c_size_t, C.c_size_t, _vp,
                                         C.c_size_t, _vp, _vp, _vp]),
+    "poporon_rng_create": (_vp, [C.c_int, _vp, C.c_size_t]),
+    "poporon_rng_destroy": (None, [_vp]),
+    "poporon_rng_next": (C.c_bool, [_vp, _vp, C.c_size_t]),
+    "poporon_amd_rng_fill_device": (C.c_bool, [_vp, _vp, C.c_size_t, _vp]),
     "poporon_amd_channel_xor_device": (C.c_bool, [_vp, _vp, C.c_size_t, _vp, C.c_size_t, C.c_size_t, _vp]),
 }
 
@@ -368,6 +372,40 @@ class Bch(Poporon):
         ok = self.lib.poporon_decode(self.h, _buf(d) if d.size else _buf(np.zeros(1, np.uint8)), d.size,
                                      _buf(p) if p.size else _buf(np.zeros(1, np.uint8)), C.byref(n))
         return bool(ok), int(n.value), d
+
+
+class Rng:
+    """poporon_rng_t (include/poporon/rng.h): xoshiro128++ seeded by splitmix32,
+    reference src/rng.c.  ``next`` fills host memory; ``fill_device`` writes
+    the same stream into device memory (poporon_amd_rng_fill_device)."""
+
+    def __init__(self, seed: int | bytes | None = 0, rng_type: int = 0):
+        self.lib = load_library()
+        if seed is None:
+            self.h = self.lib.poporon_rng_create(rng_type, None, 0)
+        else:
+            b = seed if isinstance(seed, (bytes, bytearray)) else int(seed).to_bytes(4, "little")
+            buf = np.frombuffer(bytes(b), dtype=np.uint8).copy()
+            self.h = self.lib.poporon_rng_create(rng_type, _buf(buf), buf.size)
+        if not self.h:
+            raise PoporonError("poporon_rng_create returned NULL")
+
+    def next(self, size: int) -> np.ndarray:
+        out = np.zeros(max(size, 1), np.uint8)
+        if not self.lib.poporon_rng_next(self.h, _buf(out), size):
+            raise PoporonError("poporon_rng_next failed")
+        return out[:size]
+
+    def fill_device(self, d_dest, size, stream=0):
+        if not self.lib.poporon_amd_rng_fill_device(self.h, d_dest, size, stream or None):
+            raise PoporonError(f"poporon_amd_rng_fill_device failed: {last_error()}")
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.poporon_rng_destroy(self.h)
+            self.h = None
+
+    __del__ = close
 
 
 def channel_xor_device(d_positions, d_magnitudes, per_codeword, d_codewords, stride, count, stream=0):

@@ -184,3 +184,25 @@ def test_bch_handles_and_getters():
     big = P.Bch(6, 0x43, 2)  # 63-bit codewords: created (as the reference), codec refused
     with pytest.raises(P.PoporonError, match="31 bits"):
         big.encode(np.zeros(8, np.uint8))
+
+
+def test_rng_host_api_golden():
+    """poporon_rng_create/next (include/poporon/rng.h) against the reference's
+    own output (tests/golden/rng_golden.npz, tools/gen_golden_rng.py)."""
+    import os
+    g = np.load(os.path.join(os.path.dirname(__file__), "golden", "rng_golden.npz"))
+    calls = [int(x) for x in g["calls"]]
+    i = 0
+    while f"seed{i}" in g.files:
+        sd = bytes(g[f"seed{i}"])
+        r = P.Rng(sd if sd else None)
+        got = np.concatenate([r.next(n) for n in calls])
+        assert (got == g[f"stream{i}"]).all(), i
+        i += 1
+    lib = P.load_library()
+    assert not lib.poporon_rng_next(None, None, 4)
+    r = P.Rng(1)
+    assert not lib.poporon_rng_next(r.h, None, 4)
+    buf = np.zeros(4, np.uint8)
+    assert not lib.poporon_rng_next(r.h, buf.ctypes.data_as(C.c_void_p), 0)
+    lib.poporon_rng_destroy(None)
