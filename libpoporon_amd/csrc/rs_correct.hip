@@ -526,53 +526,110 @@ __device__ __forceinline__ bool correct_one(const Gf &gf, const uint4 *__restric
         auto target = [&](uint32_t p) __attribute__((always_inline)) {
             return p < size ? data + p : (p < size + RS_NR ? parity + (p - size) : data);
         };
-        if (!ERA && pass == 1u) {
-            /* error-mode apply, two roots per step: both byte loads are
-             * issued before either root's sums, so their latencies overlap
-             * (the positions of distinct roots are distinct) */
-            for (uint32_t n = 0; n < cntmax; n += FORNEY_R) {
-                uint32_t ir[FORNEY_R], ov[FORNEY_R], lm[FORNEY_R], nm[FORNEY_R];
-                uint8_t *tg[FORNEY_R];
+        if (pass == 1u) {
+            /* apply (src/decode.c:211-227), FORNEY_R roots per step: their
+             * sums are independent (the lookups of a step issue together),
+             * and the bytes they correct are loaded one step ahead, so the
+             * HBM latency of the loads hides behind the previous step's
+             * sums.  Error mode: the root's location; erasure mode: list
+             * slot n (quirk Q1/Q2: slot by root ordinal). */
+            /* erasure mode: the slot positions, clamped to 255 (bytes
+             * >= size + 32 are never written), packed 4 per dword.  If the
+             * slots that are applied are not strictly ascending, two roots
+             * may correct the same byte: then (seq) every byte is loaded
+             * right before its store, in root order, as in the reference. */
+            uint32_t pk[RS_NR / 4];
+            bool seq = false;
+            if (ERA) {
+                bool asc = true;
+                uint32_t prev = 0, have = 0;
+#pragma unroll
+                for (int n = 0; n < RS_NR; ++n) {
+                    if ((n & 3) == 0)
+                        pk[n >> 2] = 0;
+                    if ((uint32_t)n < cntmax) { /* uniform */
+                        const uint32_t p = (uint32_t)n < cnt ? min((uint32_t)pos[n], 255u) : 255u;
+                        pk[n >> 2] |= p << (8 * (n & 3));
+                        const bool app = (uint32_t)n < cnt && p < size + RS_NR;
+                        asc = asc && !(app && have && p <= prev);
+                        prev = app ? p : prev;
+                        have |= app ? 1u : 0u;
+                    }
+                }
+                seq = wave_max(asc ? 0u : 1u) != 0u;
+            }
+            auto tpos = [&](uint32_t n, uint32_t i) __attribute__((always_inline)) {
+                if (ERA) {
+                    uint32_t w = pk[0];
+#pragma unroll
+                    for (int q = 1; q < RS_NR / 4; ++q)
+                        w = (n >> 2) == (uint32_t)q ? pk[q] : w;
+                    return (w >> (8u * (n & 3u))) & 0xffu;
+                }
+                return (uint32_t)((int32_t)((i * P.iprim + 254u) % 255u) - pad);
+            };
+            /* erasure mode loads the next step's bytes during this step's
+             * sums (measured: 1.03 -> 0.90 ms at 32 erasures); error mode
+             * loads a step's bytes at its start (the extra registers of the
+             * look-ahead spill there: 0.475 -> 0.491 ms) */
+            constexpr bool AHEAD = ERA;
+            uint32_t ir[FORNEY_R], ov[FORNEY_R];
+            if (AHEAD) {
 #pragma unroll
                 for (int t = 0; t < FORNEY_R; ++t) {
                     ir[t] = it.next(); /* 255 past the last root */
-                    tg[t] = target((uint32_t)((int32_t)((ir[t] * P.iprim + 254u) % 255u) - pad));
-                    ov[t] = *tg[t];
+                    ov[t] = seq ? 0u : *target(tpos((uint32_t)t, ir[t]));
+                }
+            }
+            for (uint32_t n = 0; n < cntmax; n += FORNEY_R) {
+                uint32_t irn[FORNEY_R], ovn[FORNEY_R], lm[FORNEY_R], nm[FORNEY_R];
+                const bool more = AHEAD && n + FORNEY_R < cntmax; /* uniform */
+                if (!AHEAD) {
+#pragma unroll
+                    for (int t = 0; t < FORNEY_R; ++t) {
+                        ir[t] = it.next();
+                        ov[t] = *target(tpos(n + (uint32_t)t, ir[t]));
+                    }
+                } else if (more) {
+#pragma unroll
+                    for (int t = 0; t < FORNEY_R; ++t) {
+                        irn[t] = it.next();
+                        ovn[t] = seq ? 0u : *target(tpos(n + FORNEY_R + (uint32_t)t, irn[t]));
+                    }
                 }
 #pragma unroll
                 for (int t = 0; t < FORNEY_R; ++t)
                     nm[t] = forney(ir[t], lm[t]);
 #pragma unroll
                 for (int t = 0; t < FORNEY_R; ++t) {
-                    const bool z = run && n + t < cnt && nm[t] != 0u;
+                    const bool z = n + t < cnt && nm[t] != 0u; /* zero numerator: no correction, not counted */
                     if (!verify) /* else counted in the check pass */
                         corrected += z ? 1u : 0u;
-                    if (z)
-                        *tg[t] = (uint8_t)(ov[t] ^ gf.exp(lm[t]));
+                    const uint32_t p = tpos(n + (uint32_t)t, ir[t]);
+                    if (z && p < size + RS_NR) {
+                        uint8_t *d = target(p);
+                        *d = (uint8_t)((seq ? (uint32_t)*d : ov[t]) ^ gf.exp(lm[t]));
+                    }
+                }
+                if (more) {
+#pragma unroll
+                    for (int t = 0; t < FORNEY_R; ++t) {
+                        ir[t] = irn[t];
+                        ov[t] = ovn[t];
+                    }
                 }
             }
         } else {
+            /* re-syndrome check (src/decode.c:193-209), per root */
             for (uint32_t n = 0; n < cntmax; ++n) {
-                const bool act = run && n < cnt;
                 const uint32_t i = it.next(); /* root, ascending as in the reference */
-                /* the byte this root corrects, loaded now so that the load's
-                 * latency overlaps the Forney sums (stored below if nonzero) */
                 const uint32_t k = (i * P.iprim + 254u) % 255u;
-                const uint32_t p = ERA ? (uint32_t)pos[n] /* quirk Q1/Q2: slot by root ordinal */
-                                       : (uint32_t)((int32_t)k - pad);
-                uint8_t *tgt = target(p);
-                const uint32_t old = pass == 1u ? (uint32_t)*tgt : 0u;
                 uint32_t lmag;
                 const uint32_t num = forney(i, lmag);
-                const uint32_t mag = gf.exp(lmag);
-                const bool nz = act && num != 0u; /* zero numerator: no correction, not counted */
-                if (nz && (verify ? pass == 0u : pass == 1u)) /* counted once, before the check */
-                    ++corrected;
-                if (pass == 1u) {
-                    if (nz && p < size + RS_NR)
-                        *tgt = (uint8_t)(old ^ mag);
-                } else if (nz) {
-                    /* re-syndrome contribution mag * alpha^((fcr+q)*prim*(254-k)) */
+                const bool nz = run && n < cnt && num != 0u;
+                if (nz) {
+                    ++corrected; /* counted once, before the check */
+                    /* contribution mag * alpha^((fcr+q)*prim*(254-k)) */
                     if (P.vfast) {
                         uint32_t e = (lmag + P.fcr * P.prim * (254u - k)) % 255u;
                         const uint32_t st = (P.prim * (254u - k)) % 255u;

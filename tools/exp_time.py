@@ -39,14 +39,41 @@ def child():
     for _ in range(3):
         step()
     torch.cuda.synchronize()
+    import time
+    t0 = time.perf_counter()
+    for _ in range(10):
+        step()
+    torch.cuda.synchronize()
+    step_ms = (time.perf_counter() - t0) / 10 * 1e3
     rs.timing(True)
     for _ in range(10):
         step()
-    res = {}
+    res = {"step_ms": round(step_ms, 4)}
     for k in (P.KERNEL_ENCODE, P.KERNEL_REMAINDER, P.KERNEL_CORRECT):
         ms, c = rs.timing_read(k)
         res[P.KERNEL_NAMES[k]] = round(ms / max(c, 1), 4)
     res["ok"] = int(ok.sum()) == n and bool((cor == 16).all())
+    rs.timing(False)
+    # erasure decode (32 sorted erasures in the data, configs[3])
+    epos, emag = bench.synth_errors(bench.SEED + 2, 0, n, 32, K, dev)
+    epos, order = epos.sort(dim=1)
+    slots = epos.to(torch.uint8).contiguous()
+    emag8 = emag.gather(1, order).to(torch.uint8).contiguous()
+    cnts = torch.full((n,), 32, dtype=torch.uint8, device=dev)
+    rs.encode_batch_device(b, N, b + K, N, K, n, s)
+
+    def estep():
+        P.channel_xor_device(slots.data_ptr(), emag8.data_ptr(), 32, b, N, n, s)
+        rs.decode_batch_device(b, N, b + K, N, K, n, ok.data_ptr(), cor.data_ptr(), d_positions=slots.data_ptr(),
+                               positions_stride=32, d_counts=cnts.data_ptr(), stream=s)
+    estep()
+    torch.cuda.synchronize()
+    rs.timing(True)
+    for _ in range(5):
+        estep()
+    ms, c = rs.timing_read(P.KERNEL_CORRECT)
+    res["erasure_correct"] = round(ms / max(c, 1), 4)
+    res["erasure_ok"] = int(ok.sum()) == n
     print(json.dumps(res))
 
 
