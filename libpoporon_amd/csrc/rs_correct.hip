@@ -350,8 +350,10 @@ __device__ __forceinline__ bool correct_one(const Gf &gf, const uint4 *__restric
     if (P.stop_at == 3u)
         return omp[0] > 3000u; /* profiling ablation */
 
-    /* derivative terms (Forney, below): Lambda_(2h+1) for 2h <= min(deg, 31) (src/decode.c:176-180) */
-    const uint32_t dtop = (deg < RS_NR - 1 ? deg : RS_NR - 1) & ~1u;
+    /* derivative terms (Forney, below): Lambda_(2h+1) for 2h <= min(deg, 31) (src/decode.c:176-180);
+     * those with 2h + 1 > deg are zero, so the terms stop at 2h <= deg - 1
+     * (16 errors: 8 terms, and Forney's powers stop at m < 16, not 17) */
+    const uint32_t dtop = (deg - 1u < RS_NR - 1 ? deg - 1u : RS_NR - 1) & ~1u;
     const uint32_t dtopmax = wave_max(dtop);
     uint32_t loddp[RS_NR / 4]; /* packed like omp: h = 2q (low), 2q+1 (high) */
 #pragma unroll
