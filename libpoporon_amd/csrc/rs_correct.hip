@@ -251,6 +251,7 @@ __device__ __forceinline__ bool correct_one(const Gf &gf, const uint4 *__restric
     for (int k = 0; k < RS_NR / 2; ++k)
         W[k] = 0xFFFFFFFFu;
     const uint32_t r0 = (ERA ? 63u - wave_max_full(63u - ne) : 0u) + 1u;
+    uint32_t ubp = 0;
     for (uint32_t r = 1; r <= RS_NR; ++r) {
 #pragma unroll
         for (int k = RS_NR / 2 - 1; k > 0; --k)
@@ -262,7 +263,9 @@ __device__ __forceinline__ bool correct_one(const Gf &gf, const uint4 *__restric
         if (r < r0) /* uniform: before the first codeword's BM step (erasure mode) */
             continue;
         const bool act = r > ne;
-        const uint32_t ub = wave_max_full(act ? dl : 0u); /* <= r - 1 */
+        /* error mode: every lane is active from r = 1, and dl only grows to
+         * the previous step's `up`, so the previous step's bound serves */
+        const uint32_t ub = (ERA || r == r0) ? wave_max_full(act ? dl : 0u) : ubp; /* <= r - 1 */
         uint32_t disc = 0;
 #pragma unroll
         for (int g = 0; g < RS_NR; g += BM_DISC_G) {
@@ -280,6 +283,7 @@ __device__ __forceinline__ bool correct_one(const Gf &gf, const uint4 *__restric
         const uint32_t dq = upd ? (uint32_t)(dd < 0 ? dd + 255 * 128 : dd) : (ZL << 7);
         const uint32_t up = min((uint32_t)RS_NR, max(dl, db + 1u));
         const uint32_t ub2 = wave_max_full(act ? up : 0u);
+        ubp = ub2;
         /* coefficients top down (index i reads the old bl[i-1] before it is
          * rewritten); groups of 4 share a uniform bound test */
 #pragma unroll
