@@ -48,6 +48,8 @@
  */
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 #include "rs_device.h"
 
 #define COR_WG 1024
@@ -335,21 +337,36 @@ __device__ __forceinline__ bool correct_one(const Gf &gf, const uint4 *__restric
      * (computed before the Chien search: it needs only Lambda and S); logs
      * packed two per register like BM's */
     uint32_t omp[RS_NR / 2];
+    /* DM > 0: the wave's maximum degree is DM (compile time: the syndromes
+     * are read once and the products of all terms interleave, no guards) */
+    auto omega = [&](auto dmc) __attribute__((always_inline)) {
+        constexpr int DM = decltype(dmc)::value;
+        uint32_t sl[DM > 0 ? DM : 1];
+        if constexpr (DM > 0) {
 #pragma unroll
-    for (int m = 0; m < RS_NR; ++m) {
-        uint32_t o = ZL;
-        if ((uint32_t)m < degmax) {
-            uint32_t acc = 0;
-#pragma unroll
-            for (int j = 0; j <= m; ++j)
-                acc ^= gf.exp(SLOG((uint32_t)(m - j)) + ll[j]);
-            o = (uint32_t)m < deg ? gf.log(acc) : ZL;
+            for (int k = 0; k < DM; ++k)
+                sl[k] = SLOG((uint32_t)k);
         }
-        if (m & 1)
-            omp[m >> 1] |= o << 16;
-        else
-            omp[m >> 1] = o;
-    }
+#pragma unroll
+        for (int m = 0; m < RS_NR; ++m) {
+            uint32_t o = ZL;
+            if (DM ? m < DM : (uint32_t)m < degmax) {
+                uint32_t acc = 0;
+#pragma unroll
+                for (int j = 0; j <= m; ++j)
+                    acc ^= gf.exp((DM ? sl[DM ? m - j : 0] : SLOG((uint32_t)(m - j))) + ll[j]);
+                o = (uint32_t)m < deg ? gf.log(acc) : ZL;
+            }
+            if (m & 1)
+                omp[m >> 1] |= o << 16;
+            else
+                omp[m >> 1] = o;
+        }
+    };
+    if (degmax == 16u)
+        omega(std::integral_constant<int, 16>{});
+    else
+        omega(std::integral_constant<int, 0>{});
 #define OMLOG(m) (((m) & 1) ? (omp[(m) >> 1] >> 16) : (omp[(m) >> 1] & 0xffffu))
     if (P.stop_at == 3u)
         return omp[0] > 3000u; /* profiling ablation */
@@ -385,6 +402,10 @@ __device__ __forceinline__ bool correct_one(const Gf &gf, const uint4 *__restric
 #pragma unroll
         for (int j = 1; j <= 16; ++j)
             ej[j] = ll[j] < ZL ? ll[j] : BIG;
+        /* DS > 0: every lane's degree bound is DS (compile time, no guards;
+         * the 16-error case: 0.462 -> 0.433 ms) */
+        auto chunks = [&](auto dsc) __attribute__((always_inline)) {
+        constexpr int DS = decltype(dsc)::value;
 #pragma unroll 1
         for (int w = 0; w < 8; ++w) {
             uint32_t word = 0;
@@ -393,10 +414,10 @@ __device__ __forceinline__ bool correct_one(const Gf &gf, const uint4 *__restric
                 uint32_t acc[4] = {0x01010101u, 0x01010101u, 0x01010101u, 0x01010101u};
 #pragma unroll
                 for (int j = 1; j <= 16; j += 2) {
-                    if ((uint32_t)j <= degsearch) {
+                    if (DS ? j <= DS : (uint32_t)j <= degsearch) {
                         const uint4 r1 = chien[(j - 1) * 256 + min(ej[j], A0)];
                         ej[j] = red(ej[j] + (16u * j) % 255u);
-                        if ((uint32_t)j + 1u <= degsearch) {
+                        if (DS ? j + 1 <= DS : (uint32_t)j + 1u <= degsearch) {
                             const uint4 r2 = chien[j * 256 + min(ej[j + 1], A0)];
                             ej[j + 1] = red(ej[j + 1] + (16u * (j + 1)) % 255u);
                             acc[0] = xor3(acc[0], r1.x, r2.x);
@@ -418,6 +439,11 @@ __device__ __forceinline__ bool correct_one(const Gf &gf, const uint4 *__restric
                 rb[q] = rb[q + 1];
             rb[7] = word;
         }
+        };
+        if (degsearch == 16u)
+            chunks(std::integral_constant<int, 16>{});
+        else
+            chunks(std::integral_constant<int, 0>{});
         rb[7] &= 0x7FFFFFFFu; /* i' = 255 repeats i' = 0 */
     } else {
         /* Karn's register form, src/decode.c:117-141 (beyond-capacity locators) */
