@@ -43,9 +43,10 @@ def main():
         slots = pos.to(torch.uint8).contiguous()
         cnt = torch.full((a.n,), 32, dtype=torch.uint8, device=dev)
         kw = dict(d_positions=slots.data_ptr(), positions_stride=32, d_counts=cnt.data_ptr())
+    pos8, mag8 = pos.to(torch.uint8).contiguous(), mag.to(torch.uint8).contiguous()
     for _ in range(a.reps):
         rs.encode_batch_device(b, N, b + K, N, K, a.n, s)
-        cw.scatter_(1, pos, cw.gather(1, pos) ^ mag)
+        P.channel_xor_device(pos8.data_ptr(), mag8.data_ptr(), pos8.shape[1], b, N, a.n, s)
         rs.decode_batch_device(b, N, b + K, N, K, a.n, ok.data_ptr(), cor.data_ptr(), stream=s, **kw)
     torch.cuda.synchronize()
     assert int(ok.sum()) == a.n, "decode failures"

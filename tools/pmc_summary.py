@@ -23,7 +23,13 @@ from collections import defaultdict
 
 NAMES = {"rs_lfsr_k<0>": "rs_lfsr_k<false> (encode)", "rs_lfsr_k<1>": "rs_lfsr_k<true> (remainder)",
          "rs_lfsr_k<2>": "rs_lfsr_k (check)", "rs_correct_k<unsigned char>": "rs_correct_k (BM/Chien/Forney)",
-         "rs_correct_k<unsigned int>": "rs_correct_k (BM/Chien/Forney, u32 slots)"}
+         "rs_correct_k<unsigned int>": "rs_correct_k (BM/Chien/Forney, u32 slots)",
+         # template <MODE, PATH> / <PosT, ERA> names of the current kernels (bench.py's keys)
+         "rs_lfsr_k<0, 0>": "rs_lfsr_k<false> (encode)", "rs_lfsr_k<0, 1>": "rs_lfsr_k<false> (encode)",
+         "rs_lfsr_k<1, 2>": "rs_lfsr_k<true> (remainder)", "rs_lfsr_k<1, 1>": "rs_lfsr_k<true> (remainder)",
+         "rs_correct_k<unsigned char, false>": "rs_correct_k (BM/Chien/Forney)",
+         "rs_correct_k<unsigned char, true>": "rs_correct_k (erasure, u8 slots)",
+         "rs_correct_k<unsigned int, true>": "rs_correct_k (erasure, u32 slots)"}
 
 
 def short(name):
