@@ -254,16 +254,23 @@ __device__ __forceinline__ bool correct_one(const Gf &gf, const uint4 *__restric
         W[k] = 0xFFFFFFFFu;
     const uint32_t r0 = (ERA ? 63u - wave_max_full(63u - ne) : 0u) + 1u;
     uint32_t ubp = 0;
-    for (uint32_t r = 1; r <= RS_NR; ++r) {
+    /* window for step r: S_(r-1) shifted in at the end of step r-1, after
+     * the update (at the head of a step it would compete with the first
+     * discrepancy group for registers and serialise its lookups) */
+    auto shift_in = [&](uint32_t r) __attribute__((always_inline)) {
 #pragma unroll
         for (int k = RS_NR / 2 - 1; k > 0; --k)
             W[k] = __builtin_amdgcn_alignbyte(W[k], W[k - 1], 2);
-        {
-            const uint32_t s8 = srow[(RS_NR - r) * COR_WG]; /* S_(r-1), byte log (255 = zero) */
-            W[0] = (W[0] << 16) | (s8 == 255u ? 0xFFFFu : s8 << 7);
-        }
-        if (r < r0) /* uniform: before the first codeword's BM step (erasure mode) */
+        const uint32_t s8 = srow[(RS_NR - r) * COR_WG]; /* S_(r-1), byte log (255 = zero) */
+        W[0] = (W[0] << 16) | (s8 == 255u ? 0xFFFFu : s8 << 7);
+    };
+    shift_in(1);
+    for (uint32_t r = 1; r <= RS_NR; ++r) {
+        if (r < r0) { /* uniform: before the first codeword's BM step (erasure mode) */
+            if (r < RS_NR)
+                shift_in(r + 1);
             continue;
+        }
         const bool act = r > ne;
         /* error mode: every lane is active from r = 1, and dl only grows to
          * the previous step's `up`, so the previous step's bound serves */
@@ -313,6 +320,8 @@ __device__ __forceinline__ bool correct_one(const Gf &gf, const uint4 *__restric
                 lb = ld;
             }
         }
+        if (r < RS_NR)
+            shift_in(r + 1);
     }
     uint32_t ll[RS_NR + 1];
 #pragma unroll
