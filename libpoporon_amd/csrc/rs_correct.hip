@@ -564,6 +564,43 @@ __device__ __forceinline__ bool correct_one(const Gf &gf, const uint4 *__restric
             lmag = (min(gf.log(num), A0) + ln2 + RS_NN - lden) % 255u;
             return num;
         };
+        /* the same for FORNEY_R roots at once, group-major: one bound test
+         * per group of powers for all the roots, whose lookups share the block */
+        auto forney_r = [&](const uint32_t (&ir)[FORNEY_R], uint32_t (&lm)[FORNEY_R], uint32_t (&nm)[FORNEY_R])
+                            __attribute__((always_inline)) {
+            uint32_t i2[FORNEY_R], ie[FORNEY_R], io[FORNEY_R], den[FORNEY_R];
+#pragma unroll
+            for (int t = 0; t < FORNEY_R; ++t) {
+                const uint32_t i1 = ir[t] == 255u ? 0u : ir[t];
+                i2[t] = red(i1 + i1);
+                ie[t] = 0;
+                io[t] = i1;
+                nm[t] = 0;
+                den[t] = 0;
+            }
+#pragma unroll
+            for (int m0 = 0; m0 < RS_NR; m0 += 4) {
+                if ((uint32_t)m0 < nir) {
+#pragma unroll
+                    for (int m = m0; m < m0 + 4; m += 2) {
+#pragma unroll
+                        for (int t = 0; t < FORNEY_R; ++t) {
+                            nm[t] ^= gf.exp(OMLOG(m) + ie[t]);
+                            den[t] ^= gf.exp(LODD(m >> 1) + ie[t]);
+                            nm[t] ^= gf.exp(OMLOG(m + 1) + io[t]);
+                            ie[t] = red(ie[t] + i2[t]);
+                            io[t] = red(io[t] + i2[t]);
+                        }
+                    }
+                }
+            }
+#pragma unroll
+            for (int t = 0; t < FORNEY_R; ++t) {
+                const uint32_t ln2 = mod255((uint32_t)((int32_t)ir[t] * ((int32_t)P.fcr - 1) + (int32_t)RS_NN));
+                const uint32_t lden = min(gf.log(den[t]), A0);
+                lm[t] = (min(gf.log(nm[t]), A0) + ln2 + RS_NN - lden) % 255u;
+            }
+        };
         auto target = [&](uint32_t p) __attribute__((always_inline)) {
             return p < size ? data + p : (p < size + RS_NR ? parity + (p - size) : data);
         };
@@ -638,9 +675,13 @@ __device__ __forceinline__ bool correct_one(const Gf &gf, const uint4 *__restric
                         ovn[t] = seq ? 0u : *target(tpos(n + FORNEY_R + (uint32_t)t, irn[t]));
                     }
                 }
+                if constexpr (!ERA) { /* group-major: 0.418 -> 0.414 ms; erasure mode root-major (0.89 vs 0.91) */
+                    forney_r(ir, lm, nm);
+                } else {
 #pragma unroll
-                for (int t = 0; t < FORNEY_R; ++t)
-                    nm[t] = forney(ir[t], lm[t]);
+                    for (int t = 0; t < FORNEY_R; ++t)
+                        nm[t] = forney(ir[t], lm[t]);
+                }
 #pragma unroll
                 for (int t = 0; t < FORNEY_R; ++t) {
                     const bool z = n + t < cnt && nm[t] != 0u; /* zero numerator: no correction, not counted */
