@@ -58,11 +58,8 @@
 #ifndef BM_DISC_G
 #define BM_DISC_G 8 /* BM discrepancy terms per branch-free group */
 #endif
-#ifndef BM_UPD_G
-#define BM_UPD_G 1  /* BM update coefficient pairs per branch-free group (measured: 1 < 2 < 4 < 8) */
-#endif
 #ifndef FORNEY_R
-#define FORNEY_R 4  /* error-mode Forney/apply: roots per step (their byte loads overlap) */
+#define FORNEY_R 4  /* Forney/apply: roots per step (their sums and byte loads overlap) */
 #endif
 #define ZL 1024u         /* log of zero (registers): exp(ZL + anything) reads past the LDS block -> 0 */
 #define BIG 0x10000000u  /* log of zero in the Chien index walk (survives 255 reductions, clamped to 255) */
