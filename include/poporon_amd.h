@@ -95,6 +95,17 @@ bool poporon_decode_batch_syndrome_device(poporon_t *pprn, uint8_t *d_data, size
                                           const uint16_t *d_syndromes, size_t syndrome_stride, uint8_t *d_ok,
                                           uint8_t *d_corrected, void *stream);
 
+/*
+ * Syndromes of a batch (the reference's calculate_syndrome_u8, src/decode.c:
+ * 375-415, per codeword): d_syndromes[c*syndrome_stride + i] = log S_i in the
+ * reference's uint16 log form (2^symbol_size - 1 = zero), d_nonzero[c] = 1
+ * when any S_i is nonzero.  Either output may be NULL (not both).  The
+ * result feeds poporon_decode_batch_syndrome_device.
+ */
+bool poporon_syndrome_batch_device(poporon_t *pprn, const uint8_t *d_data, size_t data_stride,
+                                   const uint8_t *d_parity, size_t parity_stride, size_t size, size_t count,
+                                   uint16_t *d_syndromes, size_t syndrome_stride, uint8_t *d_nonzero, void *stream);
+
 /* Screening without correction: d_dirty[c] = 1 when codeword c has a nonzero
  * syndrome (the reference's calculate_syndrome_u8 flag, src/decode.c:409-414),
  * else 0.  Reads data and parity only. */
@@ -130,13 +141,43 @@ bool poporon_amd_timing_read(poporon_t *pprn, int kernel, double *total_ms, uint
  * start states are derived on the host by GF(2) jump-ahead (rng.hip). */
 bool poporon_amd_rng_fill_device(poporon_rng_t *rng, void *d_dest, size_t size, void *stream);
 
-/* ---- test / benchmark utility (not part of the codec) ---------------------
- * Symbol-error channel: for each of count codeword rows (stride bytes apart)
- * XOR d_magnitudes[c*per_codeword + e] into byte d_positions[c*per_codeword + e]
- * of row c, in place, asynchronously on stream.  Positions within a row must
- * be distinct. */
-bool poporon_amd_channel_xor_device(const uint8_t *d_positions, const uint8_t *d_magnitudes, size_t per_codeword,
-                                    uint8_t *d_codewords, size_t stride, size_t count, void *stream);
+/* ---- multi-GPU: one handle per device, contiguous codeword ranges ----------
+ * Codewords are independent, so a batch of count codewords is split into
+ * contiguous ranges: device i (of G) takes [count*i/G, count*(i+1)/G)
+ * (poporon_amd_multi_range).  No data moves between devices.  Per-codeword
+ * results equal the single-device (and single-codeword) results.
+ *
+ * poporon_amd_multi_create makes one handle per listed device (devices NULL:
+ * every visible device) from the same config (copied; erasure / syndrome
+ * pointers borrowed as by poporon_create) and initialises each device.
+ * The host entry points take the arguments of poporon_encode_batch /
+ * poporon_decode_batch and run one host thread per device over its range.
+ * The device entry points take per-device pointer arrays: element i points to
+ * device i's range of rows in that device's memory; the work is enqueued on
+ * streams[i] (streams NULL: each device's null stream). */
+typedef struct _poporon_multi_t poporon_multi_t;
+
+poporon_multi_t *poporon_amd_multi_create(const poporon_config_t *config, const int *devices, size_t num_devices);
+void poporon_amd_multi_destroy(poporon_multi_t *multi);
+size_t poporon_amd_multi_device_count(const poporon_multi_t *multi);
+/* device i's handle (e.g. for poporon_amd_timing); owned by the multi handle */
+poporon_t *poporon_amd_multi_handle(poporon_multi_t *multi, size_t index);
+/* the range [*first, *first + *n) of part `part` out of `parts` */
+bool poporon_amd_multi_range(size_t count, size_t parts, size_t part, size_t *first, size_t *n);
+
+bool poporon_encode_batch_multi(poporon_multi_t *multi, const uint8_t *data, size_t data_stride, uint8_t *parity,
+                                size_t parity_stride, size_t size, size_t count);
+bool poporon_decode_batch_multi(poporon_multi_t *multi, uint8_t *data, size_t data_stride, uint8_t *parity,
+                                size_t parity_stride, size_t size, size_t count, const uint8_t *positions,
+                                size_t positions_stride, const uint8_t *counts, uint8_t *ok, uint8_t *corrected);
+bool poporon_encode_batch_multi_device(poporon_multi_t *multi, const uint8_t *const *d_data, size_t data_stride,
+                                       uint8_t *const *d_parity, size_t parity_stride, size_t size, size_t count,
+                                       void *const *streams);
+bool poporon_decode_batch_multi_device(poporon_multi_t *multi, uint8_t *const *d_data, size_t data_stride,
+                                       uint8_t *const *d_parity, size_t parity_stride, size_t size, size_t count,
+                                       const uint8_t *const *d_positions, size_t positions_stride,
+                                       const uint8_t *const *d_counts, uint8_t *const *d_ok,
+                                       uint8_t *const *d_corrected, void *const *streams);
 
 #ifdef __cplusplus
 }

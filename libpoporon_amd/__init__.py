@@ -88,7 +88,21 @@ _SIGS = {
     "poporon_rng_destroy": (None, [_vp]),
     "poporon_rng_next": (C.c_bool, [_vp, _vp, C.c_size_t]),
     "poporon_amd_rng_fill_device": (C.c_bool, [_vp, _vp, C.c_size_t, _vp]),
-    "poporon_amd_channel_xor_device": (C.c_bool, [_vp, _vp, C.c_size_t, _vp, C.c_size_t, C.c_size_t, _vp]),
+    "poporon_syndrome_batch_device": (C.c_bool, [_vp, _vp, C.c_size_t, _vp, C.c_size_t, C.c_size_t, C.c_size_t,
+                                                 _vp, C.c_size_t, _vp, _vp]),
+    "poporon_amd_multi_create": (_vp, [_vp, _vp, C.c_size_t]),
+    "poporon_amd_multi_destroy": (None, [_vp]),
+    "poporon_amd_multi_device_count": (C.c_size_t, [_vp]),
+    "poporon_amd_multi_handle": (_vp, [_vp, C.c_size_t]),
+    "poporon_amd_multi_range": (C.c_bool, [C.c_size_t, C.c_size_t, C.c_size_t, C.POINTER(C.c_size_t),
+                                           C.POINTER(C.c_size_t)]),
+    "poporon_encode_batch_multi": (C.c_bool, [_vp, _vp, C.c_size_t, _vp, C.c_size_t, C.c_size_t, C.c_size_t]),
+    "poporon_decode_batch_multi": (C.c_bool, [_vp, _vp, C.c_size_t, _vp, C.c_size_t, C.c_size_t, C.c_size_t, _vp,
+                                              C.c_size_t, _vp, _vp, _vp]),
+    "poporon_encode_batch_multi_device": (C.c_bool, [_vp, _vp, C.c_size_t, _vp, C.c_size_t, C.c_size_t, C.c_size_t,
+                                                     _vp]),
+    "poporon_decode_batch_multi_device": (C.c_bool, [_vp, _vp, C.c_size_t, _vp, C.c_size_t, C.c_size_t, C.c_size_t,
+                                                     _vp, C.c_size_t, _vp, _vp, _vp, _vp]),
 }
 
 # kernel ids for poporon_amd_timing_read (include/poporon_amd.h)
@@ -319,6 +333,13 @@ class Poporon:
                                                                   syndrome_stride, d_ok, d_corrected, stream or None),
                     "poporon_decode_batch_syndrome_device")
 
+    def syndrome_batch_device(self, d_data, data_stride, d_parity, parity_stride, size, count, d_syndromes,
+                              syndrome_stride, d_nonzero=None, stream=0):
+        """calculate_syndrome_u8 for a batch: u16 log-form syndromes (+ nonzero flags)."""
+        self._check(self.lib.poporon_syndrome_batch_device(self.h, d_data, data_stride, d_parity, parity_stride, size,
+                                                           count, d_syndromes, syndrome_stride, d_nonzero,
+                                                           stream or None), "poporon_syndrome_batch_device")
+
     def check_batch_device(self, d_data, data_stride, d_parity, parity_stride, size, count, d_dirty, stream=0):
         self._check(self.lib.poporon_check_batch_device(self.h, d_data, data_stride, d_parity, parity_stride, size,
                                                         count, d_dirty, stream or None), "poporon_check_batch_device")
@@ -408,15 +429,90 @@ class Rng:
     __del__ = close
 
 
-def channel_xor_device(d_positions, d_magnitudes, per_codeword, d_codewords, stride, count, stream=0):
-    """Test/benchmark channel: XOR magnitudes into positions of each codeword row (device pointers, async)."""
-    if not load_library().poporon_amd_channel_xor_device(d_positions, d_magnitudes, per_codeword, d_codewords,
-                                                         stride, count, stream or None):
-        raise PoporonError(f"poporon_amd_channel_xor_device failed: {last_error()}")
-
-
 def shard_range(count: int, rank: int, world: int):
-    """Contiguous codeword range [lo, hi) of `rank` out of `world`."""
-    per = (count + world - 1) // world
-    lo = min(count, rank * per)
-    return lo, min(count, lo + per)
+    """Contiguous codeword range [lo, hi) of `rank` out of `world`:
+    the library's own partition (poporon_amd_multi_range), [count*r/W, count*(r+1)/W)."""
+    first, n = C.c_size_t(0), C.c_size_t(0)
+    if not load_library().poporon_amd_multi_range(count, world, rank, C.byref(first), C.byref(n)):
+        raise PoporonError(f"poporon_amd_multi_range failed: {last_error()}")
+    return int(first.value), int(first.value + n.value)
+
+
+class Multi:
+    """poporon_multi_t (include/poporon_amd.h): one RS handle per device, each
+    codeword range on its own device; host batches run the devices concurrently."""
+
+    def __init__(self, devices=None, symbol_size=8, generator_polynomial=0x11D, first_consecutive_root=1,
+                 primitive_element=1, num_roots=32):
+        self.lib = load_library()
+        cfg = self.lib.poporon_rs_config_create(symbol_size, generator_polynomial, first_consecutive_root,
+                                                primitive_element, num_roots, None, None)
+        if not cfg:
+            raise PoporonError("poporon_rs_config_create returned NULL")
+        if devices is None:
+            self.h = self.lib.poporon_amd_multi_create(cfg, None, 0)
+        else:
+            arr = (C.c_int * len(devices))(*devices)
+            self.h = self.lib.poporon_amd_multi_create(cfg, arr, len(devices))
+        self.lib.poporon_config_destroy(cfg)
+        if not self.h:
+            raise PoporonError(f"poporon_amd_multi_create failed: {last_error()}")
+        self.num_roots = num_roots
+
+    @property
+    def devices(self):
+        return int(self.lib.poporon_amd_multi_device_count(self.h))
+
+    def _check(self, ok, what):
+        if not ok:
+            raise PoporonError(f"{what} failed: {last_error()}")
+
+    def encode_batch(self, data):
+        data = np.ascontiguousarray(data, dtype=np.uint8)
+        count, size = data.shape
+        par = np.zeros((count, self.num_roots), np.uint8)
+        self._check(self.lib.poporon_encode_batch_multi(self.h, _buf(data), size, _buf(par), self.num_roots, size,
+                                                        count), "poporon_encode_batch_multi")
+        return par
+
+    def decode_batch(self, data, parity, positions=None, counts=None):
+        d = np.array(data, dtype=np.uint8, copy=True, order="C")
+        p = np.array(parity, dtype=np.uint8, copy=True, order="C")
+        count, size = d.shape
+        ok = np.zeros(count, np.uint8)
+        cor = np.zeros(count, np.uint8)
+        if positions is not None:
+            pos = np.ascontiguousarray(positions, dtype=np.uint8)
+            cnt = np.ascontiguousarray(counts, dtype=np.uint8)
+            pargs = (_buf(pos), pos.shape[1], _buf(cnt))
+        else:
+            pargs = (None, 0, None)
+        self._check(self.lib.poporon_decode_batch_multi(self.h, _buf(d), size, _buf(p), p.shape[1], size, count,
+                                                        *pargs, _buf(ok), _buf(cor)), "poporon_decode_batch_multi")
+        return ok, cor, d, p
+
+    def encode_batch_device(self, d_data, data_stride, d_parity, parity_stride, size, count, streams=None):
+        """d_data / d_parity / streams: one pointer per device (device i's range of rows)."""
+        G = self.devices
+        arr = lambda v: (C.c_void_p * G)(*v)  # noqa: E731
+        self._check(self.lib.poporon_encode_batch_multi_device(self.h, arr(d_data), data_stride, arr(d_parity),
+                                                               parity_stride, size, count,
+                                                               arr(streams) if streams else None),
+                    "poporon_encode_batch_multi_device")
+
+    def decode_batch_device(self, d_data, data_stride, d_parity, parity_stride, size, count, d_ok, d_corrected=None,
+                            streams=None):
+        G = self.devices
+        arr = lambda v: (C.c_void_p * G)(*v)  # noqa: E731
+        self._check(self.lib.poporon_decode_batch_multi_device(self.h, arr(d_data), data_stride, arr(d_parity),
+                                                               parity_stride, size, count, None, 0, None, arr(d_ok),
+                                                               arr(d_corrected) if d_corrected else None,
+                                                               arr(streams) if streams else None),
+                    "poporon_decode_batch_multi_device")
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.poporon_amd_multi_destroy(self.h)
+            self.h = None
+
+    __del__ = close

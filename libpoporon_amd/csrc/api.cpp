@@ -125,8 +125,17 @@ struct GpuCtx {
     RsGenTables *gtab = nullptr; /* device (general-parameter kernels) */
     uint8_t *rem = nullptr;     /* device workspace: 32 B per codeword */
     size_t rem_cap = 0;
-    /* single-codeword staging (device) */
+    /* Ordering of the workspace across streams: rem_done is recorded on the
+     * stream of the last launch that read rem (rem_stream); a call on another
+     * stream waits for it before overwriting rem. */
+    hipEvent_t rem_done = nullptr;
+    hipStream_t rem_stream = nullptr;
+    bool rem_pending = false;
+    /* single-codeword staging: device buffer + pinned host mirror, so that a
+     * poporon_encode / poporon_decode call is one H2D copy, the kernels and
+     * one D2H copy */
     uint8_t *stage = nullptr;
+    uint8_t *hstage = nullptr;
     size_t stage_cap = 0;
     /* host-batch pipeline: PIPE_SLOTS chunks in flight, one stream each */
     struct PipeSlot {
@@ -658,15 +667,28 @@ EXPORT poporon_t *poporon_create(const poporon_config_t *config)
     return h;
 }
 
+/* Frees whatever the context holds, ready or not: a gpu_init that failed
+ * half-way leaves a stream or tables behind, and they go here so that the
+ * next call retries from scratch. */
 static void gpu_release(GpuCtx &g)
 {
-    if (!g.ready)
+    const int dev = g.device;
+    const bool any = g.ready || g.stream || g.tab || g.gtab || g.rem || g.stage || g.hstage || g.rem_done ||
+                     g.pipe[0].stream || g.pipe[1].stream || g.pipe[2].stream;
+    if (!any || dev < 0) {
+        g = GpuCtx();
+        g.device = dev;
         return;
+    }
     int prev = -1;
     (void)hipGetDevice(&prev);
-    (void)hipSetDevice(g.device);
+    (void)hipSetDevice(dev);
     if (g.stream)
         (void)hipStreamSynchronize(g.stream);
+    if (g.rem_done) {
+        (void)hipEventSynchronize(g.rem_done);
+        (void)hipEventDestroy(g.rem_done);
+    }
     for (auto &t : g.pending) {
         (void)hipEventDestroy(t.a);
         (void)hipEventDestroy(t.b);
@@ -677,6 +699,8 @@ static void gpu_release(GpuCtx &g)
     (void)hipFree(g.gtab);
     (void)hipFree(g.rem);
     (void)hipFree(g.stage);
+    if (g.hstage)
+        (void)hipHostFree(g.hstage);
     for (auto &ps : g.pipe) {
         if (ps.stream)
             (void)hipStreamSynchronize(ps.stream);
@@ -692,6 +716,7 @@ static void gpu_release(GpuCtx &g)
     if (prev >= 0)
         (void)hipSetDevice(prev);
     g = GpuCtx();
+    g.device = dev; /* a handle stays bound to the device it was given */
 }
 
 EXPORT void poporon_destroy(poporon_t *h)
@@ -770,11 +795,25 @@ EXPORT bool poporon_amd_set_device(poporon_t *h, int device)
     return true;
 }
 
+static bool gpu_init_steps(poporon_t *h);
+
+/* Lazily binds the handle to its device and uploads its tables.  A failure
+ * part-way releases what was created, so a later call can retry. */
 static bool gpu_init(poporon_t *h)
 {
-    GpuCtx &g = h->gpu;
-    if (g.ready)
+    if (h->gpu.ready)
         return true;
+    if (gpu_init_steps(h))
+        return true;
+    const std::string msg = g_last_error;
+    gpu_release(h->gpu);
+    g_last_error = msg;
+    return false;
+}
+
+static bool gpu_init_steps(poporon_t *h)
+{
+    GpuCtx &g = h->gpu;
     if (h->fec_type == PPLN_FEC_BCH && !h->bch_ok)
         return fail("BCH codewords longer than 31 bits (symbol_size > 5) are not served");
     if (h->fec_type == PPLN_FEC_RS && !h->supported)
@@ -797,6 +836,7 @@ static bool gpu_init(poporon_t *h)
     HIP_OK(hipGetDeviceProperties(&prop, g.device));
     g.num_cu = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
     HIP_OK(hipStreamCreateWithFlags(&g.stream, hipStreamNonBlocking));
+    HIP_OK(hipEventCreateWithFlags(&g.rem_done, hipEventDisableTiming));
     if (h->fec_type == PPLN_FEC_BCH) {
         /* parameters and tables go by value with every launch */
     } else if (h->fast) {
@@ -817,6 +857,10 @@ static bool ensure_rem(poporon_t *h, size_t count)
         return true;
     size_t cap = std::max(count, (size_t)1024);
     if (g.rem) {
+        /* the last reader of rem may run on any stream the caller chose */
+        if (g.rem_pending)
+            HIP_OK(hipEventSynchronize(g.rem_done));
+        g.rem_pending = false;
         HIP_OK(hipStreamSynchronize(g.stream));
         HIP_OK(hipFree(g.rem));
         g.rem = nullptr;
@@ -833,13 +877,17 @@ static bool ensure_stage(poporon_t *h, size_t bytes)
     if (g.stage_cap >= bytes)
         return true;
     size_t cap = std::max(bytes, (size_t)4096);
-    if (g.stage) {
+    if (g.stage || g.hstage) {
         HIP_OK(hipStreamSynchronize(g.stream));
         HIP_OK(hipFree(g.stage));
+        if (g.hstage)
+            HIP_OK(hipHostFree(g.hstage));
         g.stage = nullptr;
+        g.hstage = nullptr;
         g.stage_cap = 0;
     }
     HIP_OK(hipMalloc((void **)&g.stage, cap));
+    HIP_OK(hipHostMalloc((void **)&g.hstage, cap, hipHostMallocDefault));
     g.stage_cap = cap;
     return true;
 }
@@ -864,6 +912,18 @@ static size_t par_bytes(const poporon_t *h)
 static size_t kmax(const poporon_t *h)
 {
     return h->fec_type == PPLN_FEC_BCH ? (size_t)-1 : (size_t)h->rs->gf->field_size - h->rs->num_roots;
+}
+
+/* Encode sizes: the reference's uint16 byte counter never terminates past
+ * 65535 (src/encode.c:121,125, quirk Q7: refused here); a BCH message must
+ * hold the info byte image (src/encode.c:210-212). */
+static bool check_encode_size(const poporon_t *h, size_t size)
+{
+    if (h->fec_type == PPLN_FEC_BCH && size < h->bch.dbytes)
+        return fail("BCH encode size %zu < info byte image %u", size, (unsigned)h->bch.dbytes);
+    if (size > 65535)
+        return fail("size %zu > 65535 (the reference's uint16 byte counter never terminates)", size);
+    return true;
 }
 
 static bool check_decode_size(const poporon_t *h, size_t size)
@@ -966,6 +1026,25 @@ EXPORT bool poporon_amd_timing_read(poporon_t *h, int kernel, double *total_ms, 
 /* device batches                                                           */
 /* ------------------------------------------------------------------------ */
 
+/* The handle's syndrome workspace (rem) is written and read by launches on
+ * whatever stream a call names.  Before a call overwrites it, its stream waits
+ * for the last launch that read it if that ran on another stream (same stream:
+ * already ordered); after its own last reader the call records rem_done. */
+static bool rem_acquire(GpuCtx &g, hipStream_t s)
+{
+    if (g.rem_pending && g.rem_stream != s)
+        HIP_OK(hipStreamWaitEvent(s, g.rem_done, 0));
+    return true;
+}
+
+static bool rem_release(GpuCtx &g, hipStream_t s)
+{
+    HIP_OK(hipEventRecord(g.rem_done, s));
+    g.rem_stream = s;
+    g.rem_pending = true;
+    return true;
+}
+
 static bool launch_encode(poporon_t *h, const uint8_t *d_data, size_t ds, uint8_t *d_par, size_t ps, size_t size,
                           size_t count, hipStream_t s)
 {
@@ -1009,8 +1088,9 @@ static bool launch_decode(poporon_t *h, uint8_t *d_data, size_t ds, uint8_t *d_p
     RsCorrParams prm = h->corr;
     prm.size = (uint32_t)size;
     prm.pad = (int32_t)(h->rs->gf->field_size - h->rs->num_roots - size);
-    if (!rem) {
-        if (!ext_syn && !ensure_rem(h, count))
+    const bool shared = !rem && !ext_syn; /* the handle's workspace */
+    if (shared) {
+        if (!ensure_rem(h, count) || !rem_acquire(h->gpu, s))
             return false;
         rem = h->gpu.rem;
     }
@@ -1023,7 +1103,7 @@ static bool launch_decode(poporon_t *h, uint8_t *d_data, size_t ds, uint8_t *d_p
     HIP_OK(rsk_correct(h->gpu.tab, &prm, d_data, ds, d_par, ps, count, rem, ext_syn, ext_stride, pos8, pos32,
                        pos_stride, cnt, ok, corrected, h->gpu.num_cu, s));
     t.done();
-    return true;
+    return !shared || rem_release(h->gpu, s);
 }
 
 EXPORT bool poporon_check_batch_device(poporon_t *h, const uint8_t *d_data, size_t data_stride,
@@ -1047,11 +1127,49 @@ EXPORT bool poporon_check_batch_device(poporon_t *h, const uint8_t *d_data, size
     } else {
         RsGenParams prm = h->gen;
         prm.size = (uint32_t)size;
-        HIP_OK(rsg_check(h->gpu.gtab, &prm, d_data, data_stride, d_parity, parity_stride, count, d_dirty,
-                         h->gpu.num_cu, s));
+        HIP_OK(rsg_check(h->gpu.gtab, &prm, d_data, data_stride, d_parity, parity_stride, count, d_dirty, nullptr,
+                         0, h->gpu.num_cu, s));
     }
     t.done();
     return true;
+}
+
+EXPORT bool poporon_syndrome_batch_device(poporon_t *h, const uint8_t *d_data, size_t data_stride,
+                                          const uint8_t *d_parity, size_t parity_stride, size_t size, size_t count,
+                                          uint16_t *d_syndromes, size_t syndrome_stride, uint8_t *d_nonzero,
+                                          void *stream)
+{
+    if (!h || (count && (!d_data || !d_parity || (!d_syndromes && !d_nonzero))))
+        return fail("NULL argument");
+    if (h->fec_type != PPLN_FEC_RS)
+        return fail("poporon_syndrome_batch_device serves RS handles");
+    if (d_syndromes && syndrome_stride < h->rs->num_roots)
+        return fail("syndrome_stride < num_roots (%u)", (unsigned)h->rs->num_roots);
+    if (!check_decode_size(h, size))
+        return fail("size %zu outside [1, %u]", size, (unsigned)kmax(h));
+    if (!gpu_init(h))
+        return false;
+    DeviceGuard dg(h->gpu.device);
+    hipStream_t s = (hipStream_t)stream;
+    if (!h->fast) {
+        RsGenParams prm = h->gen;
+        prm.size = (uint32_t)size;
+        KernelTimer t(h->gpu, POPORON_AMD_KERNEL_REMAINDER, s);
+        HIP_OK(rsg_check(h->gpu.gtab, &prm, d_data, data_stride, d_parity, parity_stride, count, d_nonzero,
+                         d_syndromes, syndrome_stride, h->gpu.num_cu, s));
+        t.done();
+        return true;
+    }
+    if (!ensure_rem(h, count) || !rem_acquire(h->gpu, s))
+        return false;
+    {
+        KernelTimer t(h->gpu, POPORON_AMD_KERNEL_REMAINDER, s);
+        HIP_OK(rsk_syndrome(h->gpu.tab, d_data, data_stride, d_parity, parity_stride, (uint32_t)size, count,
+                            h->gpu.rem, h->gpu.num_cu, s));
+        t.done();
+    }
+    HIP_OK(rsk_syn_log(h->gpu.tab, h->gpu.rem, count, d_syndromes, syndrome_stride, d_nonzero, s));
+    return rem_release(h->gpu, s);
 }
 
 EXPORT bool poporon_encode_batch_device(poporon_t *h, const uint8_t *d_data, size_t data_stride, uint8_t *d_parity,
@@ -1059,8 +1177,8 @@ EXPORT bool poporon_encode_batch_device(poporon_t *h, const uint8_t *d_data, siz
 {
     if (!h || (count && (!d_data || !d_parity)))
         return fail("NULL argument");
-    if (size > 65535)
-        return fail("size %zu > 65535 (the reference's uint16 byte counter never terminates)", size);
+    if (!check_encode_size(h, size))
+        return false;
     if (!gpu_init(h))
         return false;
     DeviceGuard dg(h->gpu.device);
@@ -1186,8 +1304,8 @@ EXPORT bool poporon_encode_batch(poporon_t *h, const uint8_t *data, size_t data_
 {
     if (!h || (count && (!data || !parity)))
         return fail("NULL argument");
-    if (size > 65535)
-        return fail("size %zu > 65535", size);
+    if (!check_encode_size(h, size))
+        return false;
     if (!gpu_init(h))
         return false;
     DeviceGuard dg(h->gpu.device);
@@ -1318,6 +1436,177 @@ EXPORT bool poporon_decode_batch(poporon_t *h, uint8_t *data, size_t data_stride
 }
 
 /* ------------------------------------------------------------------------ */
+/* multi-GPU: one handle per device, contiguous codeword ranges             */
+/* ------------------------------------------------------------------------ */
+
+/*
+ * Codewords are independent: a batch is split into
+ * contiguous ranges, device i taking [count*i/G, count*(i+1)/G), and no data
+ * crosses between devices.  Each device has its own handle (tables,
+ * workspace, streams); the host entry points run one host thread per device,
+ * each driving its handle's pinned pipeline over its range, so the devices'
+ * PCIe links and kernels work concurrently.
+ */
+struct _poporon_multi_t {
+    std::vector<poporon_t *> h;
+};
+
+EXPORT bool poporon_amd_multi_range(size_t count, size_t parts, size_t part, size_t *first, size_t *n)
+{
+    if (parts == 0 || part >= parts || !first || !n)
+        return fail("bad partition arguments");
+    /* 128-bit products: count * part may exceed 64 bits for huge counts */
+    const size_t a = (size_t)(((unsigned __int128)count * part) / parts);
+    const size_t b = (size_t)(((unsigned __int128)count * (part + 1)) / parts);
+    *first = a;
+    *n = b - a;
+    return true;
+}
+
+EXPORT void poporon_amd_multi_destroy(poporon_multi_t *m)
+{
+    if (!m)
+        return;
+    for (auto *p : m->h)
+        poporon_destroy(p);
+    delete m;
+}
+
+EXPORT poporon_multi_t *poporon_amd_multi_create(const poporon_config_t *config, const int *devices,
+                                                 size_t num_devices)
+{
+    if (!config)
+        return nullptr;
+    std::vector<int> devs;
+    if (devices) {
+        devs.assign(devices, devices + num_devices);
+    } else {
+        const int n = poporon_amd_device_count();
+        for (int d = 0; d < n; d++)
+            devs.push_back(d);
+    }
+    if (devs.empty()) {
+        fail("no HIP device for the multi-GPU handle");
+        return nullptr;
+    }
+    poporon_multi_t *m = new (std::nothrow) _poporon_multi_t();
+    if (!m)
+        return nullptr;
+    for (size_t i = 0; i < devs.size(); i++) {
+        for (size_t j = 0; j < i; j++) {
+            if (devs[j] == devs[i]) {
+                fail("device %d listed twice", devs[i]);
+                poporon_amd_multi_destroy(m);
+                return nullptr;
+            }
+        }
+        poporon_t *p = poporon_create(config);
+        if (!p || !poporon_amd_set_device(p, devs[i]) || !gpu_init(p)) {
+            const std::string msg = g_last_error;
+            poporon_destroy(p);
+            poporon_amd_multi_destroy(m);
+            fail("device %d: %s", devs[i], msg.c_str());
+            return nullptr;
+        }
+        m->h.push_back(p);
+    }
+    return m;
+}
+
+EXPORT size_t poporon_amd_multi_device_count(const poporon_multi_t *m) { return m ? m->h.size() : 0; }
+
+EXPORT poporon_t *poporon_amd_multi_handle(poporon_multi_t *m, size_t index)
+{
+    return (m && index < m->h.size()) ? m->h[index] : nullptr;
+}
+
+/* run f(i, first, n) for every device's range, one host thread per device;
+ * the first failure's message is kept */
+template <class F>
+static bool multi_run(poporon_multi_t *m, size_t count, F &&f)
+{
+    const size_t G = m->h.size();
+    std::vector<std::string> err(G);
+    std::vector<char> okv(G, 1);
+    std::vector<std::thread> th;
+    auto one = [&](size_t i) {
+        size_t first = 0, n = 0;
+        poporon_amd_multi_range(count, G, i, &first, &n);
+        if (n && !f(i, first, n)) {
+            okv[i] = 0;
+            err[i] = g_last_error;
+        }
+    };
+    for (size_t i = 1; i < G; i++)
+        th.emplace_back(one, i);
+    one(0);
+    for (auto &t : th)
+        t.join();
+    for (size_t i = 0; i < G; i++)
+        if (!okv[i])
+            return fail("device %zu: %s", i, err[i].c_str());
+    return true;
+}
+
+EXPORT bool poporon_encode_batch_multi(poporon_multi_t *m, const uint8_t *data, size_t data_stride, uint8_t *parity,
+                                       size_t parity_stride, size_t size, size_t count)
+{
+    if (!m || (count && (!data || !parity)))
+        return fail("NULL argument");
+    return multi_run(m, count, [&](size_t i, size_t c0, size_t n) {
+        return poporon_encode_batch(m->h[i], data + c0 * data_stride, data_stride, parity + c0 * parity_stride,
+                                    parity_stride, size, n);
+    });
+}
+
+EXPORT bool poporon_decode_batch_multi(poporon_multi_t *m, uint8_t *data, size_t data_stride, uint8_t *parity,
+                                       size_t parity_stride, size_t size, size_t count, const uint8_t *positions,
+                                       size_t positions_stride, const uint8_t *counts, uint8_t *ok,
+                                       uint8_t *corrected)
+{
+    if (!m || (count && (!data || !parity || !ok)))
+        return fail("NULL argument");
+    return multi_run(m, count, [&](size_t i, size_t c0, size_t n) {
+        return poporon_decode_batch(m->h[i], data + c0 * data_stride, data_stride, parity + c0 * parity_stride,
+                                    parity_stride, size, n, positions ? positions + c0 * positions_stride : nullptr,
+                                    positions_stride, counts ? counts + c0 : nullptr, ok + c0,
+                                    corrected ? corrected + c0 : nullptr);
+    });
+}
+
+/* Device-resident shards: device i's range (poporon_amd_multi_range) sits at
+ * the i-th pointer of each array, in that device's memory; enqueued on
+ * streams[i] (streams may be NULL: each device's null stream).  Returns once
+ * every device's work is enqueued. */
+EXPORT bool poporon_encode_batch_multi_device(poporon_multi_t *m, const uint8_t *const *d_data, size_t data_stride,
+                                              uint8_t *const *d_parity, size_t parity_stride, size_t size,
+                                              size_t count, void *const *streams)
+{
+    if (!m || (count && (!d_data || !d_parity)))
+        return fail("NULL argument");
+    return multi_run(m, count, [&](size_t i, size_t, size_t n) {
+        return poporon_encode_batch_device(m->h[i], d_data[i], data_stride, d_parity[i], parity_stride, size, n,
+                                           streams ? streams[i] : nullptr);
+    });
+}
+
+EXPORT bool poporon_decode_batch_multi_device(poporon_multi_t *m, uint8_t *const *d_data, size_t data_stride,
+                                              uint8_t *const *d_parity, size_t parity_stride, size_t size,
+                                              size_t count, const uint8_t *const *d_positions,
+                                              size_t positions_stride, const uint8_t *const *d_counts,
+                                              uint8_t *const *d_ok, uint8_t *const *d_corrected, void *const *streams)
+{
+    if (!m || (count && (!d_data || !d_parity || !d_ok)))
+        return fail("NULL argument");
+    return multi_run(m, count, [&](size_t i, size_t, size_t n) {
+        return poporon_decode_batch_device(m->h[i], d_data[i], data_stride, d_parity[i], parity_stride, size, n,
+                                           d_positions ? d_positions[i] : nullptr, positions_stride,
+                                           d_counts ? d_counts[i] : nullptr, d_ok[i],
+                                           d_corrected ? d_corrected[i] : nullptr, streams ? streams[i] : nullptr);
+    });
+}
+
+/* ------------------------------------------------------------------------ */
 /* single-codeword API (the reference's entry points): a batch of one       */
 /* ------------------------------------------------------------------------ */
 
@@ -1336,15 +1625,19 @@ EXPORT bool poporon_encode(poporon_t *h, uint8_t *data, size_t size, uint8_t *pa
     DeviceGuard dg(h->gpu.device);
     GpuCtx &g = h->gpu;
     const size_t nr = par_bytes(h);
-    if (!ensure_stage(h, size + nr + 16))
+    const size_t off_p = (size + 15) & ~(size_t)15;
+    if (!ensure_stage(h, off_p + nr + 16))
         return false;
-    uint8_t *dd = g.stage, *dp = g.stage + ((size + 15) & ~(size_t)15);
-    if (size)
-        HIP_OK(hipMemcpyAsync(dd, data, size, hipMemcpyHostToDevice, g.stream));
-    if (!launch_encode(h, dd, size, dp, nr, size, 1, g.stream))
+    /* pinned mirror: one H2D copy in, one D2H copy out */
+    if (size) {
+        memcpy(g.hstage, data, size);
+        HIP_OK(hipMemcpyAsync(g.stage, g.hstage, size, hipMemcpyHostToDevice, g.stream));
+    }
+    if (!launch_encode(h, g.stage, size, g.stage + off_p, nr, size, 1, g.stream))
         return false;
-    HIP_OK(hipMemcpyAsync(parity, dp, nr, hipMemcpyDeviceToHost, g.stream));
+    HIP_OK(hipMemcpyAsync(g.hstage + off_p, g.stage + off_p, nr, hipMemcpyDeviceToHost, g.stream));
     HIP_OK(hipStreamSynchronize(g.stream));
+    memcpy(parity, g.hstage + off_p, nr);
     return true;
 }
 
@@ -1412,46 +1705,49 @@ EXPORT bool poporon_decode(poporon_t *h, uint8_t *data, size_t size, uint8_t *pa
         const size_t off_x = (off_cor + 1 + 15) & ~(size_t)15;
         if (!ensure_stage(h, off_x + nr * 4 + 16))
             return false;
-        std::vector<uint8_t> hostbuf(nr * 4 + 16, 0);
+        /* everything goes through the pinned mirror: one H2D copy of
+         * [data | parity | ok | cor | pad | syndromes or slots + count], the
+         * kernels, one D2H copy of [data | parity | ok | cor] */
+        uint8_t *hs = g.hstage;
         const uint16_t *ext = nullptr;
         const uint32_t *pos32 = nullptr;
         const uint8_t *cnt = nullptr;
         bool refuse = false;
-        HIP_OK(hipMemcpyAsync(g.stage, data, size, hipMemcpyHostToDevice, g.stream));
-        HIP_OK(hipMemcpyAsync(g.stage + off_p, parity, nr, hipMemcpyHostToDevice, g.stream));
+        size_t in_bytes = off_cor + 1;
+        memcpy(hs, data, size);
+        memcpy(hs + off_p, parity, nr);
         if (h->ext_syndrome) {
             for (size_t i = 0; i < nr; i++)
                 refuse |= h->ext_syndrome[i] > h->rs->gf->field_size; /* out-of-table index in the reference */
-            memcpy(hostbuf.data(), h->ext_syndrome, nr * sizeof(uint16_t));
-            HIP_OK(hipMemcpyAsync(g.stage + off_x, hostbuf.data(), nr * sizeof(uint16_t), hipMemcpyHostToDevice,
-                                  g.stream));
+            memcpy(hs + off_x, h->ext_syndrome, nr * sizeof(uint16_t));
+            in_bytes = off_x + nr * sizeof(uint16_t);
             ext = (const uint16_t *)(g.stage + off_x);
         } else if (h->erasure) {
             const poporon_erasure_t *e = h->erasure;
             /* the reference reads slots by root ordinal (quirks Q2/Q3): copy nr
              * slots, those past the list's capacity read as 0 */
-            memcpy(hostbuf.data(), e->erasure_positions, std::min<size_t>(e->capacity, nr) * sizeof(uint32_t));
+            memset(hs + off_x, 0, nr * 4);
+            memcpy(hs + off_x, e->erasure_positions, std::min<size_t>(e->capacity, nr) * sizeof(uint32_t));
             if (e->erasure_count > nr)
                 refuse = true; /* quirk Q5: overflows the locator in the reference */
-            hostbuf[nr * 4] = (uint8_t)std::min<uint32_t>(e->erasure_count, 255u);
-            HIP_OK(hipMemcpyAsync(g.stage + off_x, hostbuf.data(), nr * 4 + 1, hipMemcpyHostToDevice, g.stream));
+            hs[off_x + nr * 4] = (uint8_t)std::min<uint32_t>(e->erasure_count, 255u);
+            in_bytes = off_x + nr * 4 + 1;
             pos32 = (const uint32_t *)(g.stage + off_x);
             cnt = g.stage + off_x + nr * 4;
         }
         if (refuse) {
-            HIP_OK(hipStreamSynchronize(g.stream));
             fail("erasure count > num_roots or external syndrome > field size: undefined in the reference, refused");
         } else {
+            HIP_OK(hipMemcpyAsync(g.stage, hs, in_bytes, hipMemcpyHostToDevice, g.stream));
             if (!launch_decode(h, g.stage, size, g.stage + off_p, nr, size, 1, ext, nr, nullptr, pos32, nr, cnt,
                                g.stage + off_ok, g.stage + off_cor, g.stream))
                 return false;
-            uint8_t res[2];
-            HIP_OK(hipMemcpyAsync(data, g.stage, size, hipMemcpyDeviceToHost, g.stream));
-            HIP_OK(hipMemcpyAsync(parity, g.stage + off_p, nr, hipMemcpyDeviceToHost, g.stream));
-            HIP_OK(hipMemcpyAsync(res, g.stage + off_ok, 2, hipMemcpyDeviceToHost, g.stream));
+            HIP_OK(hipMemcpyAsync(hs, g.stage, off_cor + 1, hipMemcpyDeviceToHost, g.stream));
             HIP_OK(hipStreamSynchronize(g.stream));
-            success = res[0] != 0;
-            fixed = res[1];
+            memcpy(data, hs, size);
+            memcpy(parity, hs + off_p, nr);
+            success = hs[off_ok] != 0;
+            fixed = hs[off_cor];
         }
     }
     h->last_corrected = fixed;

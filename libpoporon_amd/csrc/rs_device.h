@@ -77,6 +77,11 @@ hipError_t rsk_encode(const RsDevTables *tab, const uint8_t *data, size_t dstrid
 hipError_t rsk_syndrome(const RsDevTables *tab, const uint8_t *data, size_t dstride, const uint8_t *parity,
                         size_t pstride, uint32_t size, size_t count, uint8_t *syn, int num_cu, hipStream_t stream);
 
+/* poly syndromes (32 B per codeword, rsk_syndrome) -> log form: out[c*stride + i]
+ * = log S_i (255 = zero), flag[c] = any S_i nonzero; out / flag may be NULL */
+hipError_t rsk_syn_log(const RsDevTables *tab, const uint8_t *syn, size_t count, uint16_t *out, size_t stride,
+                       uint8_t *flag, hipStream_t stream);
+
 /* flag[c] = remainder of codeword c is nonzero */
 hipError_t rsk_check(const RsDevTables *tab, const uint8_t *data, size_t dstride, const uint8_t *parity, size_t pstride,
                      uint32_t size, size_t count, uint8_t *flag, int num_cu, hipStream_t stream);

@@ -41,9 +41,11 @@ hipError_t rsg_decode(const RsGenTables *tab, const RsGenParams *prm, uint8_t *d
                       const uint32_t *pos32, size_t pos_stride, const uint8_t *cnt, uint8_t *ok, uint8_t *corrected,
                       int num_cu, hipStream_t stream);
 
+/* dirty[c] = any syndrome nonzero (may be NULL); syn (may be NULL): the
+ * nroots log-form syndromes of codeword c at syn[c*syn_stride ..] */
 hipError_t rsg_check(const RsGenTables *tab, const RsGenParams *prm, const uint8_t *data, size_t dstride,
-                     const uint8_t *parity, size_t pstride, size_t count, uint8_t *dirty, int num_cu,
-                     hipStream_t stream);
+                     const uint8_t *parity, size_t pstride, size_t count, uint8_t *dirty, uint16_t *syn,
+                     size_t syn_stride, int num_cu, hipStream_t stream);
 
 #ifdef __cplusplus
 }

@@ -387,15 +387,22 @@ __global__ __launch_bounds__(G_WG_MAX) void rsg_decode_k(const RsGenTables *__re
 __global__ __launch_bounds__(G_WG_MAX) void rsg_check_k(const RsGenTables *__restrict__ T, RsGenParams P,
                                                          const uint8_t *__restrict__ data, size_t dstride,
                                                          const uint8_t *__restrict__ parity, size_t pstride,
-                                                         size_t count, uint8_t *__restrict__ dirty)
+                                                         size_t count, uint8_t *__restrict__ dirty,
+                                                         uint16_t *__restrict__ syn, size_t syn_stride)
 {
     extern __shared__ uint8_t smem[];
     const GShared s = g_setup(T, smem);
     const GMod mod{P.nn, P.magic};
     const LaneArr S{s.arr(0, P.nroots + 1u) + threadIdx.x, s.wg};
     for (size_t cw = (size_t)blockIdx.x * blockDim.x + threadIdx.x; cw < count;
-         cw += (size_t)gridDim.x * blockDim.x)
-        dirty[cw] = g_syndromes(s, mod, P, data + cw * dstride, parity + cw * pstride, S) ? 1 : 0;
+         cw += (size_t)gridDim.x * blockDim.x) {
+        const bool nz = g_syndromes(s, mod, P, data + cw * dstride, parity + cw * pstride, S);
+        if (dirty)
+            dirty[cw] = nz ? 1 : 0;
+        if (syn) /* log form, the reference's uint16 array (src/decode.c:409-412) */
+            for (uint32_t i = 0; i < P.nroots; ++i)
+                syn[cw * syn_stride + i] = S[i];
+    }
 }
 
 /* ------------------------------------------------------------------------ */
@@ -454,8 +461,8 @@ extern "C" hipError_t rsg_decode(const RsGenTables *tab, const RsGenParams *prm,
 }
 
 extern "C" hipError_t rsg_check(const RsGenTables *tab, const RsGenParams *prm, const uint8_t *data, size_t dstride,
-                                const uint8_t *parity, size_t pstride, size_t count, uint8_t *dirty, int num_cu,
-                                hipStream_t stream)
+                                const uint8_t *parity, size_t pstride, size_t count, uint8_t *dirty, uint16_t *syn,
+                                size_t syn_stride, int num_cu, hipStream_t stream)
 {
     if (count == 0)
         return hipSuccess;
@@ -463,6 +470,6 @@ extern "C" hipError_t rsg_check(const RsGenTables *tab, const RsGenParams *prm, 
     size_t lds;
     g_shape(*prm, 1, wg, lds);
     hipLaunchKernelGGL(rsg_check_k, g_grid(count, wg, num_cu, lds), dim3(wg), lds, stream, tab, *prm, data, dstride,
-                       parity, pstride, count, dirty);
+                       parity, pstride, count, dirty, syn, syn_stride);
     return hipGetLastError();
 }

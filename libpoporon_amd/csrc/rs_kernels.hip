@@ -521,6 +521,39 @@ extern "C" hipError_t rsk_syndrome(const RsDevTables *tab, const uint8_t *data, 
     return launch_lfsr<MODE_SYNDROME>(tab, data, dstride, parity, pstride, size, count, syn, num_cu, stream);
 }
 
+/* poly-form syndromes (rsk_syndrome's output) -> the reference's log form:
+ * uint16 log S_i (255 = zero) and the "any nonzero" flag (src/decode.c:409-414) */
+__global__ __launch_bounds__(256) void rs_synlog_k(const RsDevTables *__restrict__ T, const uint8_t *__restrict__ syn,
+                                                   size_t count, uint16_t *__restrict__ out, size_t stride,
+                                                   uint8_t *__restrict__ flag)
+{
+    __shared__ uint8_t lg[256];
+    lg[threadIdx.x] = T->log[threadIdx.x];
+    __syncthreads();
+    const size_t cw = (size_t)blockIdx.x * 256u + threadIdx.x;
+    if (cw >= count)
+        return;
+    uint32_t any = 0;
+    for (uint32_t i = 0; i < RS_NR; ++i) {
+        const uint32_t v = syn[cw * RS_NR + i];
+        any |= v;
+        if (out)
+            out[cw * stride + i] = lg[v];
+    }
+    if (flag)
+        flag[cw] = any != 0u;
+}
+
+extern "C" hipError_t rsk_syn_log(const RsDevTables *tab, const uint8_t *syn, size_t count, uint16_t *out,
+                                  size_t stride, uint8_t *flag, hipStream_t stream)
+{
+    if (count == 0)
+        return hipSuccess;
+    const size_t blocks = (count + 255) / 256;
+    hipLaunchKernelGGL(rs_synlog_k, dim3((uint32_t)blocks), dim3(256), 0, stream, tab, syn, count, out, stride, flag);
+    return hipGetLastError();
+}
+
 extern "C" hipError_t rsk_check(const RsDevTables *tab, const uint8_t *data, size_t dstride, const uint8_t *parity,
                                 size_t pstride, uint32_t size, size_t count, uint8_t *flag, int num_cu,
                                 hipStream_t stream)

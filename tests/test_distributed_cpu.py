@@ -1,69 +1,101 @@
-"""Multi-process (gloo, world size 2) checks of the N>1 bookkeeping of bench.py.
+"""Multi-process (gloo) tests of bench.py's multi-rank path, on CPU.
 
-The GPU path shards codewords by contiguous global ranges with no data-path
-collective; here, on CPU: every rank generates its shard from the global
-index (counter hash) and the concatenation equals the single-process data;
-errors likewise; max-time and sum reductions behave as bench.py uses them.
+`bench.py --gpus N` starts N ranks itself (torch.distributed.run as a child
+process, before any GPU use).  Here the same launcher, the configs[4] strong
+split (libpoporon_amd's partition), the weak-scaling shard offsets and the
+rank reductions run with tests/bench_cpu_backend.py, which replaces the HIP
+codec by the CPU oracle.  The configs[4] checksum must be identical for every
+rank count, and n_gpus must equal --gpus.
 """
+import json
 import os
-import socket
+import subprocess
+import sys
 
+import numpy as np
 import pytest
-import torch
-import torch.distributed as dist
-import torch.multiprocessing as mp
 
 import bench
 import libpoporon_amd as P
+import testutil as T
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def _free_port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    port = s.getsockname()[1]
-    s.close()
-    return port
+def _run(gpus, extra=(), env_extra=None):
+    env = dict(os.environ)
+    env["PYTHONPATH"] = ROOT + os.pathsep + env.get("PYTHONPATH", "")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    env.update(env_extra or {})
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(gpus), "--backend", "tests.bench_cpu_backend",
+           "--batch", "256", "--steps", "1", "--warmup", "0", "--c4-total", "1000", "--c4-chunk", "300",
+           "--c4-reps", "1", *extra]
+    return subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=600, cwd=ROOT)
 
 
-def _worker(rank, world, port, total, q):
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
-    lo, hi = P.shard_range(total, rank, world)
-    data = bench.synth_bytes(bench.SEED, lo, hi - lo, 223, "cpu")
-    pos, mag = bench.synth_errors(bench.SEED + 1, lo, hi - lo, 16, 255, "cpu")
-    t = bench.allreduce(float(rank + 1), dist.ReduceOp.MAX, world, device="cpu")
-    s = bench.allreduce(float(hi - lo), dist.ReduceOp.SUM, world, device="cpu")
-    q.put((rank, data.numpy().copy(), pos.numpy().copy(), mag.numpy().copy(), t, s))
-    dist.barrier()
-    dist.destroy_process_group()
+def _line(r):
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [x for x in r.stdout.splitlines() if x.startswith("{")]
+    assert len(lines) == 1, r.stdout[-3000:]
+    return json.loads(lines[0])
 
 
-@pytest.mark.parametrize("total", [1000, 1 << 12])
-def test_two_rank_sharding_matches_single(total):
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, total, q)) for r in range(2)]
-    for p in procs:
-        p.start()
-    res = sorted([q.get(timeout=120) for _ in procs], key=lambda x: x[0])
-    for p in procs:
-        p.join(timeout=60)
-        assert p.exitcode == 0
-    full = bench.synth_bytes(bench.SEED, 0, total, 223, "cpu").numpy()
-    fpos, fmag = bench.synth_errors(bench.SEED + 1, 0, total, 16, 255, "cpu")
-    import numpy as np
-    assert (np.concatenate([r[1] for r in res]) == full).all()
-    assert (np.concatenate([r[2] for r in res]) == fpos.numpy()).all()
-    assert (np.concatenate([r[3] for r in res]) == fmag.numpy()).all()
-    assert all(r[4] == 2.0 for r in res)          # max over ranks
-    assert all(r[5] == float(total) for r in res)  # sum of shard sizes
+def test_launcher_ranks_and_checksum():
+    one = _line(_run(1))
+    two = _line(_run(2))
+    assert one["n_gpus"] == 1 and two["n_gpus"] == 2
+    assert one["verified"] and two["verified"]
+    # configs[4]: the same 1000 codewords however they are split
+    assert one["configs4"]["codewords_per_gpu"] == 1000 and two["configs4"]["codewords_per_gpu"] == 500
+    assert one["parity_checksum"] == two["parity_checksum"] == one["configs4"]["parity_checksum"]
+    from oracle import Oracle
+    msgs = T.synth_rows_cpu(bench.SEED + 4, 0, 1000, 223)
+    cw = np.concatenate([msgs, Oracle().encode_batch(msgs)], 1)
+    assert T.checksum_cpu(cw, 0) == one["parity_checksum"]
+    # weak scaling: rank r owns rows [r*B, (r+1)*B), the line counts both ranks
+    assert two["config"]["codewords_per_gpu"] == 256
+    msgs2 = T.synth_rows_cpu(bench.SEED, 0, 512, 223)
+    cw2 = np.concatenate([msgs2, Oracle().encode_batch(msgs2)], 1)
+    assert T.checksum_cpu(cw2, 0) == two["weak_checksum"]
 
 
-def test_error_positions_unique_and_in_range():
-    pos, mag = bench.synth_errors(bench.SEED + 1, 123, 512, 16, 255, "cpu")
+def test_gpus_must_match_world_size():
+    r = _run(1, env_extra={"WORLD_SIZE": "2", "RANK": "0", "LOCAL_RANK": "0"})
+    assert r.returncode != 0 and "WORLD_SIZE=2" in (r.stderr + r.stdout)
+
+
+@pytest.mark.parametrize("total,world", [(1000, 2), (4096, 3), (1 << 20, 8), (7, 8)])
+def test_partition_matches_library(total, world):
+    """bench.shard is the library's partition (poporon_amd_multi_range)."""
+    got = [bench.shard(total, r, world) for r in range(world)]
+    assert got == [P.shard_range(total, r, world) for r in range(world)]
+    assert got[0][0] == 0 and got[-1][1] == total
+    assert all(got[i][1] == got[i + 1][0] for i in range(world - 1))
+
+
+def test_shards_reproduce_single_process_rows():
+    """Rows, errors and checksums depend only on the global row index."""
+    total, world = 1000, 3
+    full = T.synth_rows_cpu(bench.SEED, 0, total, 223)
+    fpos, fmag = T.synth_errors_cpu(bench.SEED + 1, 0, total, 16, 255)
+    parts = [bench.shard(total, r, world) for r in range(world)]
+    assert (np.concatenate([T.synth_rows_cpu(bench.SEED, a, b - a, 223) for a, b in parts]) == full).all()
+    ep = [T.synth_errors_cpu(bench.SEED + 1, a, b - a, 16, 255) for a, b in parts]
+    assert (np.concatenate([e[0] for e in ep]) == fpos).all() and (np.concatenate([e[1] for e in ep]) == fmag).all()
+    cs = sum(T.checksum_cpu(full[a:b], a) for a, b in parts) & ((1 << 64) - 1)
+    assert cs == T.checksum_cpu(full, 0)
+
+
+def test_error_patterns_unique_and_in_range():
+    pos, mag = T.synth_errors_cpu(bench.SEED + 1, 123, 512, 16, 255)
     assert int(pos.min()) >= 0 and int(pos.max()) < 255
     assert all(len(set(row.tolist())) == 16 for row in pos)
     assert int(mag.min()) >= 1
-    epos, _ = bench.synth_errors(bench.SEED + 2, 0, 256, 32, 223, "cpu")
+    epos, emag = T.synth_errors_cpu(bench.SEED + 2, 0, 256, 32, 223, sorted_positions=True)
     assert int(epos.max()) < 223 and all(len(set(r.tolist())) == 32 for r in epos)
+    assert (np.diff(epos.astype(np.int32), axis=1) > 0).all()
+    # sorting keeps each magnitude with its position
+    up, um = T.synth_errors_cpu(bench.SEED + 2, 0, 256, 32, 223)
+    for r in range(256):
+        assert dict(zip(up[r].tolist(), um[r].tolist())) == dict(zip(epos[r].tolist(), emag[r].tolist()))

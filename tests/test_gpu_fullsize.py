@@ -1,0 +1,285 @@
+"""GPU tests: full-size configurations, the syndrome API, multi-GPU C ABI,
+workspace ordering across streams, the test utilities and the compiled C
+drop-in programs.  Everything goes through libpoporon_amd.so (C ABI).
+
+Full sizes use size-independent properties (every codeword decodes back to
+the encoded word with ok = 1 and corrected = 16 / 32; an order-independent
+checksum of the decoded batch equals that of the encoded batch) plus a
+1-in-4096 sample compared bit for bit with the CPU oracle.
+"""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+import libpoporon_amd as P
+import testutil as T
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+K, NR, N = 223, 32, 255
+SEED = 0x5EED0001
+
+
+@pytest.fixture(scope="module")
+def torch_cuda():
+    import torch
+    assert torch.cuda.is_available()
+    return torch
+
+
+@pytest.fixture(scope="module")
+def rs():
+    if P.device_count() == 0:
+        pytest.fail("no HIP device: GPU tests must run on the MI355X box")
+    return P.Poporon.default()
+
+
+def _stream(torch):
+    return torch.cuda.current_stream().cuda_stream
+
+
+def _checksum(torch, rows, first=0):
+    s = torch.zeros(1, dtype=torch.int64, device="cuda")
+    T.checksum(rows.data_ptr(), N, N, first, rows.shape[0], s.data_ptr(), _stream(torch))
+    return int(s.item()) & ((1 << 64) - 1)
+
+
+def _synth(torch, n, seed=SEED, first=0):
+    rows = torch.empty((n, N), dtype=torch.uint8, device="cuda")
+    T.synth_rows(seed, first, n, K, rows.data_ptr(), N, _stream(torch))
+    return rows
+
+
+def _errors(torch, n, nerr, span, seed, sorted_positions=False, first=0):
+    pos = torch.empty((n, nerr), dtype=torch.uint8, device="cuda")
+    mag = torch.empty((n, nerr), dtype=torch.uint8, device="cuda")
+    T.synth_errors(seed, first, n, nerr, span, pos.data_ptr(), mag.data_ptr(), sorted_positions, _stream(torch))
+    return pos, mag
+
+
+# ---------------------------------------------------------------------------
+# test utilities: the HIP kernels equal their numpy restatements
+# ---------------------------------------------------------------------------
+def test_testutil_matches_numpy(torch_cuda):
+    torch = torch_cuda
+    n, first = 3000, 123457
+    rows = _synth(torch, n, first=first)
+    torch.cuda.synchronize()
+    host = rows.cpu().numpy()
+    assert (host[:, :K] == T.synth_rows_cpu(SEED, first, n, K)).all()
+    for nerr, span, srt in ((16, 255, False), (32, 223, True), (5, 17, False)):
+        pos, mag = _errors(torch, n, nerr, span, SEED + 9, srt, first=first)
+        torch.cuda.synchronize()
+        wp, wm = T.synth_errors_cpu(SEED + 9, first, n, nerr, span, srt)
+        assert (pos.cpu().numpy() == wp).all() and (mag.cpu().numpy() == wm).all(), (nerr, span, srt)
+    host[:, K:] = np.random.default_rng(1).integers(0, 256, (n, NR), dtype=np.uint8)
+    rows.copy_(torch.from_numpy(host).cuda())
+    pos, mag = _errors(torch, n, 16, 255, SEED + 1, first=first)
+    T.channel_xor(pos.data_ptr(), mag.data_ptr(), 16, rows.data_ptr(), N, n, _stream(torch))
+    torch.cuda.synchronize()
+    want = T.channel_xor_cpu(host, pos.cpu().numpy(), mag.cpu().numpy())
+    assert (rows.cpu().numpy() == want).all()
+    assert _checksum(torch, rows, first) == T.checksum_cpu(want, first)
+
+
+# ---------------------------------------------------------------------------
+# syndromes (calculate_syndrome_u8 per codeword) against the reference
+# ---------------------------------------------------------------------------
+def _syndromes(torch, h, rows_np, size, nr):
+    n = rows_np.shape[0]
+    t = torch.from_numpy(np.ascontiguousarray(rows_np)).cuda()
+    syn = torch.zeros((n, nr), dtype=torch.int16, device="cuda")  # uint16 bit patterns
+    nz = torch.zeros(n, dtype=torch.uint8, device="cuda")
+    w = size + nr
+    h.syndrome_batch_device(t.data_ptr(), w, t.data_ptr() + size, w, size, n, syn.data_ptr(), nr, nz.data_ptr(),
+                            _stream(torch))
+    torch.cuda.synchronize()
+    return syn.cpu().numpy().astype(np.uint16), nz.cpu().numpy()
+
+
+def test_syndromes_golden(rs, golden, torch_cuda):
+    """The kernel's syndromes equal the ones the compiled reference computed
+    for every golden decode case (dec_syn: u16 log form, 255 = zero)."""
+    sizes = golden["dec_size"]
+    for s in np.unique(sizes):
+        sel = np.nonzero(sizes == s)[0]
+        s = int(s)
+        syn, nz = _syndromes(torch_cuda, rs, golden["dec_in"][sel, :s + NR], s, NR)
+        want = golden["dec_syn"][sel]
+        assert (syn == want).all(), s
+        assert (nz == (want != 255).any(axis=1)).all(), s
+
+
+@pytest.mark.parametrize("params", [(8, 0x11D, 1, 1, 32), (8, 0x187, 112, 11, 32), (8, 0x11D, 1, 1, 16),
+                                    (6, 0x43, 1, 1, 10), (4, 0x13, 1, 2, 8)])
+def test_syndromes_vs_oracle(torch_cuda, params):
+    from oracle import Oracle
+    m, poly, fcr, prim, nr = params
+    o, h = Oracle(*params), P.Poporon(*params)
+    nn = (1 << m) - 1
+    rng = np.random.default_rng(sum(params))
+    for size in (nn - nr, max(1, (nn - nr) // 3)):
+        data = rng.integers(0, nn + 1, (500, size), dtype=np.uint8)
+        cw = np.concatenate([data, o.encode_batch(data)], 1)
+        for c in range(1, 500):
+            ne = c % (nr + 3)
+            p = rng.permutation(size + nr)[:ne]
+            cw[c, p] ^= rng.integers(1, nn + 1, ne).astype(np.uint8)
+        syn, nz = _syndromes(torch_cuda, h, cw, size, nr)
+        for c in range(500):
+            f, s = o.syndrome(cw[c, :size], cw[c, size:])
+            assert (syn[c] == s).all() and bool(nz[c]) == f, (size, c)
+
+
+# ---------------------------------------------------------------------------
+# one handle, two streams: the syndrome workspace is ordered across streams
+# ---------------------------------------------------------------------------
+def test_one_handle_two_streams(torch_cuda):
+    """Back-to-back decode_batch_device calls of ONE handle on two streams
+    share the handle's workspace; the second call's stream waits for the
+    first call's last reader (poporon_amd.h), so both batches decode right."""
+    torch = torch_cuda
+    h = P.Poporon.default()
+    n = 1 << 18
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    bufs, cleans, sts = [], [], []
+    for k in range(2):
+        rows = _synth(torch, n, seed=SEED + 20 + k)
+        b = rows.data_ptr()
+        h.encode_batch_device(b, N, b + K, N, K, n, _stream(torch))
+        cleans.append(rows.clone())
+        pos, mag = _errors(torch, n, 16, N, SEED + 30 + k)
+        T.channel_xor(pos.data_ptr(), mag.data_ptr(), 16, b, N, n, _stream(torch))
+        bufs.append(rows)
+        sts.append((torch.zeros(n, dtype=torch.uint8, device="cuda"), torch.zeros(n, dtype=torch.uint8, device="cuda")))
+    torch.cuda.synchronize()
+    for k, s in enumerate((s1, s2)):  # enqueued back to back, no host sync in between
+        b = bufs[k].data_ptr()
+        h.decode_batch_device(b, N, b + K, N, K, n, sts[k][0].data_ptr(), sts[k][1].data_ptr(), stream=s.cuda_stream)
+    torch.cuda.synchronize()
+    for k in range(2):
+        assert bool((sts[k][0] == 1).all()) and bool((sts[k][1] == 16).all())
+        assert torch.equal(bufs[k], cleans[k])
+
+
+# ---------------------------------------------------------------------------
+# full sizes: configs[4]'s per-GPU share at 8 GPUs (2^23), all of configs[4]
+# on one GPU (2^26 codewords, 16.3 GB), configs[3] at 2^20
+# ---------------------------------------------------------------------------
+@pytest.mark.parametrize("n", [1 << 23, 1 << 26])
+def test_full_size_roundtrip(rs, oracle_default, torch_cuda, n):
+    torch = torch_cuda
+    rows = _synth(torch, n, seed=SEED + 4)
+    b = rows.data_ptr()
+    s = _stream(torch)
+    rs.encode_batch_device(b, N, b + K, N, K, n, s)
+    torch.cuda.synchronize()
+    sample = rows[::4096].cpu().numpy()
+    assert (oracle_default.encode_batch(sample[:, :K]) == sample[:, K:]).all()
+    clean_sum = _checksum(torch, rows)
+    pos, mag = _errors(torch, n, 16, N, SEED + 5)
+    T.channel_xor(pos.data_ptr(), mag.data_ptr(), 16, b, N, n, s)
+    del pos, mag
+    torch.cuda.synchronize()
+    bad_sample = rows[::4096].cpu().numpy()
+    ok = torch.zeros(n, dtype=torch.uint8, device="cuda")
+    cor = torch.zeros(n, dtype=torch.uint8, device="cuda")
+    rs.decode_batch_device(b, N, b + K, N, K, n, ok.data_ptr(), cor.data_ptr(), stream=s)
+    torch.cuda.synchronize()
+    assert int((ok != 1).sum()) == 0
+    assert int((cor != 16).sum()) == 0
+    assert _checksum(torch, rows) == clean_sum
+    ook, ocor, od, op = oracle_default.decode_batch(bad_sample[:, :K], bad_sample[:, K:])
+    got = rows[::4096].cpu().numpy()
+    assert (ook == 1).all() and (ocor == 16).all()
+    assert (got[:, :K] == od).all() and (got[:, K:] == op).all()
+
+
+def test_erasure_full_size(rs, oracle_default, torch_cuda):
+    """configs[3]: 2^20 codewords, 32 sorted erasures in [0, 223) each."""
+    torch = torch_cuda
+    n = 1 << 20
+    rows = _synth(torch, n, seed=SEED + 6)
+    b = rows.data_ptr()
+    s = _stream(torch)
+    rs.encode_batch_device(b, N, b + K, N, K, n, s)
+    torch.cuda.synchronize()
+    clean_sum = _checksum(torch, rows)
+    slots, mag = _errors(torch, n, 32, K, SEED + 2, sorted_positions=True)
+    T.channel_xor(slots.data_ptr(), mag.data_ptr(), 32, b, N, n, s)
+    torch.cuda.synchronize()
+    bad_sample = rows[::4096].cpu().numpy()
+    slot_sample = slots[::4096].cpu().numpy()
+    cnt = torch.full((n,), 32, dtype=torch.uint8, device="cuda")
+    ok = torch.zeros(n, dtype=torch.uint8, device="cuda")
+    cor = torch.zeros(n, dtype=torch.uint8, device="cuda")
+    rs.decode_batch_device(b, N, b + K, N, K, n, ok.data_ptr(), cor.data_ptr(), d_positions=slots.data_ptr(),
+                           positions_stride=32, d_counts=cnt.data_ptr(), stream=s)
+    torch.cuda.synchronize()
+    assert int((ok != 1).sum()) == 0 and int((cor != 32).sum()) == 0
+    assert _checksum(torch, rows) == clean_sum
+    m = bad_sample.shape[0]
+    ook, ocor, od, op = oracle_default.decode_batch(bad_sample[:, :K], bad_sample[:, K:], slot_sample.astype(np.uint32),
+                                                    np.full(m, 32, np.uint32))
+    got = rows[::4096].cpu().numpy()
+    assert (got[:, :K] == od).all() and (got[:, K:] == op).all() and (ocor == 32).all()
+
+
+# ---------------------------------------------------------------------------
+# multi-GPU C ABI (every visible device; one on the test box)
+# ---------------------------------------------------------------------------
+def test_multi_device_api(oracle_default, torch_cuda):
+    torch = torch_cuda
+    m = P.Multi()
+    G = m.devices
+    assert G == P.device_count() >= 1
+    rng = np.random.default_rng(404)
+    n = 20000
+    data = rng.integers(0, 256, (n, K), dtype=np.uint8)
+    par = m.encode_batch(data)
+    assert (par == oracle_default.encode_batch(data)).all()
+    cw = np.concatenate([data, par], 1)
+    for c in range(n):
+        ne = c % 20
+        p = rng.permutation(N)[:ne]
+        cw[c, p] ^= rng.integers(1, 256, ne, dtype=np.uint8)
+    ok, cor, d, p = m.decode_batch(cw[:, :K], cw[:, K:])
+    ook, ocor, od, op = oracle_default.decode_batch(cw[:, :K], cw[:, K:])
+    assert (ok == ook).all() and (cor == ocor).all() and (d == od).all() and (p == op).all()
+    # device-resident shards: device i holds rows [first_i, first_i + n_i)
+    shards, oks, cors, ptrs = [], [], [], []
+    for i in range(G):
+        lo, hi = P.shard_range(n, i, G)
+        with torch.cuda.device(i):
+            t = torch.from_numpy(np.ascontiguousarray(cw[lo:hi])).to(f"cuda:{i}")
+            shards.append(t)
+            oks.append(torch.zeros(hi - lo, dtype=torch.uint8, device=f"cuda:{i}"))
+            cors.append(torch.zeros(hi - lo, dtype=torch.uint8, device=f"cuda:{i}"))
+    for i in range(G):
+        torch.cuda.synchronize(i)
+    m.decode_batch_device([t.data_ptr() for t in shards], N, [t.data_ptr() + K for t in shards], N, K, n,
+                          [o.data_ptr() for o in oks], [c.data_ptr() for c in cors])
+    for i in range(G):
+        torch.cuda.synchronize(i)
+    out = np.concatenate([t.cpu().numpy() for t in shards])
+    assert (np.concatenate([o.cpu().numpy() for o in oks]) == ook).all()
+    assert (np.concatenate([c.cpu().numpy() for c in cors]) == ocor).all()
+    assert (out[:, :K] == od).all() and (out[:, K:] == op).all()
+    m.close()
+
+
+# ---------------------------------------------------------------------------
+# compiled C drop-in programs (tests/c): the reference's README example and
+# its RS codec assertions, linked against libpoporon_amd.so
+# ---------------------------------------------------------------------------
+def test_c_dropin_programs():
+    d = os.path.join(ROOT, "tests", "c")
+    r = subprocess.run([os.path.join(d, "readme_example")], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    assert "Corrected 2 errors" in r.stdout and "Decoded: Hello, Reed-Solomon!" in r.stdout
+    r = subprocess.run([os.path.join(d, "test_rs_api")], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr + r.stdout
+    assert "all checks passed" in r.stdout

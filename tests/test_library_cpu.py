@@ -206,3 +206,52 @@ def test_rng_host_api_golden():
     buf = np.zeros(4, np.uint8)
     assert not lib.poporon_rng_next(r.h, buf.ctypes.data_as(C.c_void_p), 0)
     lib.poporon_rng_destroy(None)
+
+
+def test_c_dropin_builds_and_checks_arguments():
+    """tests/c/test_rs_api.c compiles against include/poporon.h alone, links
+    libpoporon_amd.so and passes the reference's argument checks
+    (tests/test_codec.c:69-71, :220-223) without a GPU."""
+    import os
+    import subprocess
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    subprocess.check_call(["make", "-s", "-C", os.path.join(root, "tests", "c")])
+    r = subprocess.run([os.path.join(root, "tests", "c", "test_rs_api"), "--no-gpu"], capture_output=True, text=True,
+                       timeout=60)
+    assert r.returncode == 0, r.stderr
+    assert "all checks passed" in r.stdout
+
+
+def test_multi_partition_and_argument_checks(lib):
+    first, n = C.c_size_t(0), C.c_size_t(0)
+    for count in (0, 5, 1000, (1 << 26) + 7):
+        for parts in (1, 2, 3, 8):
+            spans = []
+            for p in range(parts):
+                assert lib.poporon_amd_multi_range(count, parts, p, C.byref(first), C.byref(n))
+                spans.append((first.value, first.value + n.value))
+            assert spans[0][0] == 0 and spans[-1][1] == count
+            assert all(spans[i][1] == spans[i + 1][0] for i in range(parts - 1))
+            assert max(b - a for a, b in spans) - min(b - a for a, b in spans) <= 1
+    assert not lib.poporon_amd_multi_range(10, 0, 0, C.byref(first), C.byref(n))
+    assert not lib.poporon_amd_multi_range(10, 2, 2, C.byref(first), C.byref(n))
+    assert lib.poporon_amd_multi_device_count(None) == 0
+    assert not lib.poporon_amd_multi_handle(None, 0)
+    lib.poporon_amd_multi_destroy(None)
+    assert not lib.poporon_encode_batch_multi(None, None, 0, None, 0, 223, 1)
+    if P.device_count() == 0:
+        cfg = lib.poporon_config_rs_default()
+        assert not lib.poporon_amd_multi_create(cfg, None, 0)  # no device: NULL, with a message
+        assert "no HIP device" in P.last_error()
+        lib.poporon_config_destroy(cfg)
+
+
+def test_syndrome_api_argument_checks(lib):
+    h = P.Poporon.default()
+    assert not lib.poporon_syndrome_batch_device(h.h, None, 255, None, 255, 223, 4, None, 32, None, None)
+    assert not lib.poporon_syndrome_batch_device(None, None, 255, None, 255, 223, 0, None, 32, None, None)
+    b = P.Bch.default()
+    x = np.zeros(64, np.uint8)
+    xp = x.ctypes.data_as(C.c_void_p)
+    assert not lib.poporon_syndrome_batch_device(b.h, xp, 3, xp, 3, 1, 1, xp, 32, None, None)
+    assert "RS handles" in P.last_error()

@@ -12,7 +12,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 import torch  # noqa: E402
 
-import bench  # noqa: E402
+import bench
+import devdata  # noqa: E402
 import libpoporon_amd as P  # noqa: E402
 
 
@@ -21,12 +22,12 @@ def main():
     n, K, N = 1 << 20, 223, 255
     dev = torch.device("cuda", 0)
     cw0 = torch.zeros((n, N), dtype=torch.uint8, device=dev)
-    cw0[:, :K] = bench.synth_bytes(bench.SEED, 0, n, K, dev)
+    cw0[:, :K] = devdata.synth_bytes(bench.SEED, 0, n, K, dev)
     if erasure:
-        pos, mag = bench.synth_errors(bench.SEED + 2, 0, n, 32, K, dev)
+        pos, mag = devdata.synth_errors(bench.SEED + 2, 0, n, 32, K, dev)
         pos = pos.sort(dim=1).values
     else:
-        pos, mag = bench.synth_errors(bench.SEED + 1, 0, n, 16, N, dev)
+        pos, mag = devdata.synth_errors(bench.SEED + 1, 0, n, 16, N, dev)
     ok = torch.zeros(n, dtype=torch.uint8, device=dev)
     cor = torch.zeros(n, dtype=torch.uint8, device=dev)
     s = torch.cuda.current_stream().cuda_stream

@@ -14,7 +14,8 @@ sys.path.insert(0, ROOT)
 
 import torch  # noqa: E402
 
-import bench  # noqa: E402
+import bench
+import devdata  # noqa: E402
 import libpoporon_amd as P  # noqa: E402
 
 
@@ -29,16 +30,16 @@ def main():
     rs.reserve(a.n)
     K, N = 223, 255
     cw = torch.zeros((a.n, N), dtype=torch.uint8, device=dev)
-    cw[:, :K] = bench.synth_bytes(bench.SEED, 0, a.n, K, dev)
+    cw[:, :K] = devdata.synth_bytes(bench.SEED, 0, a.n, K, dev)
     ok = torch.zeros(a.n, dtype=torch.uint8, device=dev)
     cor = torch.zeros(a.n, dtype=torch.uint8, device=dev)
     s = torch.cuda.current_stream().cuda_stream
     b = cw.data_ptr()
     if a.mode == "roundtrip":
-        pos, mag = bench.synth_errors(bench.SEED + 1, 0, a.n, 16, N, dev)
+        pos, mag = devdata.synth_errors(bench.SEED + 1, 0, a.n, 16, N, dev)
         kw = {}
     else:
-        pos, mag = bench.synth_errors(bench.SEED + 2, 0, a.n, 32, K, dev)
+        pos, mag = devdata.synth_errors(bench.SEED + 2, 0, a.n, 32, K, dev)
         pos = pos.sort(dim=1).values
         slots = pos.to(torch.uint8).contiguous()
         cnt = torch.full((a.n,), 32, dtype=torch.uint8, device=dev)
@@ -46,7 +47,7 @@ def main():
     pos8, mag8 = pos.to(torch.uint8).contiguous(), mag.to(torch.uint8).contiguous()
     for _ in range(a.reps):
         rs.encode_batch_device(b, N, b + K, N, K, a.n, s)
-        P.channel_xor_device(pos8.data_ptr(), mag8.data_ptr(), pos8.shape[1], b, N, a.n, s)
+        devdata.channel(pos8, mag8, pos8.shape[1], b, N, a.n, s)
         rs.decode_batch_device(b, N, b + K, N, K, a.n, ok.data_ptr(), cor.data_ptr(), stream=s, **kw)
     torch.cuda.synchronize()
     assert int(ok.sum()) == a.n, "decode failures"
