@@ -126,11 +126,23 @@ bool poporon_decode_batch(poporon_t *pprn, uint8_t *data, size_t data_stride, ui
  * recorded on the stream it runs on.  poporon_amd_timing(pprn, 1) enables and
  * resets the totals; poporon_amd_timing_read waits for the recorded events and
  * returns the summed kernel time (ms) and launch count for one kernel id:
- * 0 = encode LFSR, 1 = remainder LFSR, 2 = correction, 3 = check LFSR. */
+ * 0 = encode LFSR, 1 = remainder LFSR, 2 = correction (single kernel),
+ * 3 = check LFSR; the split error-mode decode of large batches: 4 = BM +
+ * Omega, 5 = Chien, 6 = Forney, 8 = apply, 7 = the general kernel over the
+ * codewords the split kernels hand on.
+ *
+ * Error-mode batches of at least 8192 codewords (no erasures, no external
+ * syndromes) take the split decode; POPORON_AMD_DECODE_PATH=split / single
+ * in the environment at poporon_create forces one or the other. */
 #define POPORON_AMD_KERNEL_ENCODE 0
 #define POPORON_AMD_KERNEL_REMAINDER 1
 #define POPORON_AMD_KERNEL_CORRECT 2
 #define POPORON_AMD_KERNEL_CHECK 3
+#define POPORON_AMD_KERNEL_BM 4
+#define POPORON_AMD_KERNEL_CHIEN 5
+#define POPORON_AMD_KERNEL_FORNEY 6
+#define POPORON_AMD_KERNEL_LIST 7
+#define POPORON_AMD_KERNEL_APPLY 8
 bool poporon_amd_timing(poporon_t *pprn, int enable);
 bool poporon_amd_timing_read(poporon_t *pprn, int kernel, double *total_ms, uint64_t *launches);
 

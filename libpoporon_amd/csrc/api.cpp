@@ -105,7 +105,7 @@ struct _poporon_config_t {
     uint8_t correction_capability; /* BCH */
 };
 
-#define NKERN 4
+#define NKERN 9
 struct TimedLaunch {
     int kernel;
     hipEvent_t a, b;
@@ -115,15 +115,15 @@ struct GpuCtx {
     bool timing = false;
     std::vector<TimedLaunch> pending;
     std::vector<hipEvent_t> event_pool;
-    double total_ms[NKERN] = {0, 0, 0, 0};
-    uint64_t launches[NKERN] = {0, 0, 0, 0};
+    double total_ms[NKERN] = {};
+    uint64_t launches[NKERN] = {};
     bool ready = false;
     int device = -1;
     int num_cu = 256;
     hipStream_t stream = nullptr;
     RsDevTables *tab = nullptr; /* device (fast kernels) */
     RsGenTables *gtab = nullptr; /* device (general-parameter kernels) */
-    uint8_t *rem = nullptr;     /* device workspace: 32 B per codeword */
+    uint8_t *rem = nullptr;     /* device workspace: rs_ws_bytes(rem_cap) (rs_device.h) */
     size_t rem_cap = 0;
     /* Ordering of the workspace across streams: rem_done is recorded on the
      * stream of the last launch that read rem (rem_stream); a call on another
@@ -159,6 +159,7 @@ struct _poporon_t {
     size_t last_corrected;
     bool supported; /* fast || generic */
     bool fast;      /* served by the RS(255,223) kernels (rs_kernels.hip, rs_correct.hip) */
+    int decode_path; /* 0: by batch size, 1: split kernels (rs_fast.hip), 2: single kernel */
     bool generic;   /* served by the general-parameter kernels (rs_generic.hip) */
     RsDevTables host_tab;
     RsCorrParams corr;
@@ -485,6 +486,8 @@ static void build_tables(poporon_t *h)
     p.force_verify = (fv && fv[0] == '1') ? 1u : 0u;
     const char *sa = getenv("POPORON_AMD_STOP_AT"); /* profiling ablation only */
     p.stop_at = sa ? (uint32_t)atoi(sa) : 0u;
+    const char *dp = getenv("POPORON_AMD_DECODE_PATH");
+    h->decode_path = dp && !strcmp(dp, "split") ? 1 : (dp && !strcmp(dp, "single") ? 2 : 0);
 }
 
 /* General-parameter kernels: byte symbols (2 <= m <= 8) and 1 <= num_roots
@@ -866,7 +869,7 @@ static bool ensure_rem(poporon_t *h, size_t count)
         g.rem = nullptr;
         g.rem_cap = 0;
     }
-    HIP_OK(hipMalloc((void **)&g.rem, cap * RS_NR));
+    HIP_OK(hipMalloc((void **)&g.rem, rs_ws_bytes(cap)));
     g.rem_cap = cap;
     return true;
 }
@@ -1062,10 +1065,57 @@ static bool launch_encode(poporon_t *h, const uint8_t *d_data, size_t ds, uint8_
     return true;
 }
 
+/* error-mode batches from this size on take the split kernels (rs_fast.hip:
+ * five launches instead of two, each at twice the occupancy) */
+#define SPLIT_MIN_COUNT 8192
+
+/* the split error-mode decode of one sub-batch (rs_fast.hip) */
+static bool launch_split(poporon_t *h, const RsCorrParams &prm, const RsSplitWs &ws, uint8_t *d_data, size_t ds,
+                         uint8_t *d_par, size_t ps, size_t size, size_t count, uint8_t *ok, uint8_t *corrected,
+                         hipStream_t s)
+{
+    GpuCtx &g = h->gpu;
+    {
+        KernelTimer t(g, POPORON_AMD_KERNEL_REMAINDER, s);
+        HIP_OK(rsk_syndrome_reset(g.tab, d_data, ds, d_par, ps, (uint32_t)size, count, ws.syn, ws.nlist, g.num_cu,
+                                  s));
+        t.done();
+    }
+    {
+        KernelTimer t(g, POPORON_AMD_KERNEL_BM, s);
+        HIP_OK(rsk_bm(g.tab, &ws, count, ok, corrected, g.num_cu, s));
+        t.done();
+    }
+    {
+        KernelTimer t(g, POPORON_AMD_KERNEL_CHIEN, s);
+        HIP_OK(rsk_chien(g.tab, &prm, &ws, count, ok, corrected, g.num_cu, s));
+        t.done();
+    }
+    {
+        KernelTimer t(g, POPORON_AMD_KERNEL_FORNEY, s);
+        HIP_OK(rsk_forney(g.tab, &prm, &ws, d_data, ds, d_par, ps, count, ok, corrected, g.num_cu, s));
+        t.done();
+    }
+    if (prm.stop_at != 5u) { /* 5: profiling ablation, no apply */
+        KernelTimer t(g, POPORON_AMD_KERNEL_APPLY, s);
+        HIP_OK(rsk_apply(&prm, &ws, d_data, ds, d_par, ps, count, s));
+        t.done();
+    }
+    {
+        KernelTimer t(g, POPORON_AMD_KERNEL_LIST, s);
+        HIP_OK(rsk_correct_list(g.tab, &prm, d_data, ds, d_par, ps, count, ws.syn, ws.list, ws.nlist, ok,
+                                corrected, g.num_cu, s));
+        t.done();
+    }
+    return true;
+}
+
+/* rem / rem_cap: a workspace of rs_ws_bytes(rem_cap) bytes (rem_cap >= count)
+ * owned by the caller; NULL: the handle's own */
 static bool launch_decode(poporon_t *h, uint8_t *d_data, size_t ds, uint8_t *d_par, size_t ps, size_t size,
                           size_t count, const uint16_t *ext_syn, size_t ext_stride, const uint8_t *pos8,
                           const uint32_t *pos32, size_t pos_stride, const uint8_t *cnt, uint8_t *ok,
-                          uint8_t *corrected, hipStream_t s, uint8_t *rem = nullptr)
+                          uint8_t *corrected, hipStream_t s, uint8_t *rem = nullptr, size_t rem_cap = 0)
 {
     if (h->fec_type == PPLN_FEC_BCH) {
         if (ext_syn || pos8 || pos32)
@@ -1093,6 +1143,19 @@ static bool launch_decode(poporon_t *h, uint8_t *d_data, size_t ds, uint8_t *d_p
         if (!ensure_rem(h, count) || !rem_acquire(h->gpu, s))
             return false;
         rem = h->gpu.rem;
+        rem_cap = h->gpu.rem_cap;
+    }
+    const bool split = !ext_syn && !pos8 && !pos32 && prm.vfast && !prm.force_verify && (!prm.stop_at || prm.stop_at >= 5) &&
+                       h->decode_path != 2 && (h->decode_path == 1 || count >= SPLIT_MIN_COUNT);
+    if (split) {
+        const RsSplitWs ws = rs_ws_carve(rem, rem_cap ? rem_cap : count);
+        GpuCtx &g = h->gpu;
+        /* (sub-batches of 2^19 codewords, to keep a sub-batch's bytes in the
+         * Infinity Cache until the apply, measured slower: 0.84 vs 0.75 ms
+         * per bench step) */
+        if (!launch_split(h, prm, ws, d_data, ds, d_par, ps, size, count, ok, corrected, s))
+            return false;
+        return !shared || rem_release(g, s);
     }
     if (!ext_syn) {
         KernelTimer t(h->gpu, POPORON_AMD_KERNEL_REMAINDER, s);
@@ -1368,12 +1431,12 @@ EXPORT bool poporon_decode_batch(poporon_t *h, uint8_t *data, size_t data_stride
     const size_t nr = par_bytes(h);
     const size_t w = size + nr;
     const size_t chunk = std::max<size_t>(1, std::min(count, kPipeChunk));
-    /* slot layout: [codewords w*n | ok n | cor n | positions nr*n | counts n | syndrome workspace 32*n (device)] */
-    const size_t per = w + 2 + (positions ? nr + 1 : 0) + RS_NR;
+    /* slot layout: [codewords w*n | ok n | cor n | positions nr*n | counts n | decode workspace (device)] */
+    const size_t per = w + 2 + (positions ? nr + 1 : 0);
     /* parity right after the data in rows of equal stride: move whole rows */
     const bool rows = parity == data + size && parity_stride == data_stride;
     for (auto &ps : g.pipe)
-        if (!pipe_slot(h, ps, chunk * per + 256))
+        if (!pipe_slot(h, ps, chunk * per + 256 + rs_ws_bytes(chunk)))
             return false;
     auto finish = [&](GpuCtx::PipeSlot &ps) -> bool {
         if (!ps.busy)
@@ -1418,7 +1481,8 @@ EXPORT bool poporon_decode_batch(poporon_t *h, uint8_t *data, size_t data_stride
                (!positions || hipMemcpyAsync(dc + o_pos, hc + o_pos, n * nr + n, hipMemcpyHostToDevice,
                                              ps.stream) == hipSuccess) &&
                launch_decode(h, dc, w, dc + size, w, size, n, nullptr, 0, positions ? dc + o_pos : nullptr, nullptr,
-                             nr, positions ? dc + o_cnt : nullptr, dc + o_ok, dc + o_cor, ps.stream, dc + o_rem) &&
+                             nr, positions ? dc + o_cnt : nullptr, dc + o_ok, dc + o_cor, ps.stream, dc + o_rem,
+                             n) &&
                hipMemcpyAsync(hc, dc, n * w + 2 * n, hipMemcpyDeviceToHost, ps.stream) == hipSuccess &&
                hipEventRecord(ps.done, ps.stream) == hipSuccess;
         ps.busy = true;

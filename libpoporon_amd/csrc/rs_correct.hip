@@ -48,9 +48,11 @@
  */
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <type_traits>
 
 #include "rs_device.h"
+#include "rs_lane.h"
 
 #define COR_WG 1024
 #define GF_REPL 32
@@ -70,123 +72,19 @@
 #define LDS_END (LDS_GF + 512u * GF_REPL * 4u)
 static_assert(LDS_END == 163840u, "lgf must end exactly at the end of the 160 KiB LDS allocation");
 
-typedef __attribute__((address_space(3))) const uint8_t lds_u8;
-
 struct Gf {
-    const uint8_t *p; /* lgf + (lane & 31) * 4 + 1: this lane's copy of the exp byte of entry 0 */
+    uint32_t pa; /* LDS byte address of this lane's copy of the exp byte of entry 0: lgf + (lane & 31) * 4 + 1 */
     /* alpha^x for x < 511; 0 for x >= 511 (exp2[511] = 0, past it the allocation ends) -- x < 2^24 */
-    __device__ __forceinline__ uint32_t exp(uint32_t x) const { return p[x * (GF_REPL * 4)]; }
+    __device__ __forceinline__ uint32_t exp(uint32_t x) const { return lds8(pa + x * (GF_REPL * 4)); }
     /* scaled log of v < 256: 128 log v, 0xFFFF for v = 0 */
-    __device__ __forceinline__ uint32_t logs(uint32_t v) const
-    {
-        return *reinterpret_cast<const uint16_t *>(p + v * (GF_REPL * 4) + 1);
-    }
+    __device__ __forceinline__ uint32_t logs(uint32_t v) const { return lds16(pa + v * (GF_REPL * 4) + 1); }
     /* log of v < 256; 511 for v = 0 (exp of 511 + anything is 0) */
     __device__ __forceinline__ uint32_t log(uint32_t v) const { return logs(v) >> 7; }
-    /* "address-form" logs (BM): a = 128 log v + (p - LDS base), zero = 0xFFFF + (p - LDS base):
-     * the exp byte of a plus a scaled log s is at LDS byte a + s */
-    __device__ __forceinline__ uint32_t expa(uint32_t a) const { return *(lds_u8 *)(size_t)a; }
-    /* LDS byte address of p (the base of address-form logs) */
-    __device__ __forceinline__ uint32_t pofs() const { return (uint32_t)(size_t)(lds_u8 *)p; }
-};
-
-/* gf_mod of src/internal/common.h:102-110 on the uint16 truncation of v */
-__device__ __forceinline__ uint32_t mod255(uint32_t v) { return (v & 0xffffu) % 255u; }
-/* x < 510 -> x mod 255; sentinel x >= 767 -> x - 255 (still >= 512) */
-__device__ __forceinline__ uint32_t red(uint32_t x) { return min(x, x - 255u); }
-/* stored byte log (255 = zero) -> register log: max(s, (s - 254) * 1024) as
- * signed ints is s for s <= 254 and 1024 for 255 (mad + max, no compare) */
-__device__ __forceinline__ uint32_t conv(uint32_t s8)
-{
-    return (uint32_t)max((int32_t)s8, ((int32_t)s8 - 254) * (int32_t)ZL);
-}
-
-/* u16 halves of packed log pairs: entry 2k low, 2k+1 high */
-__device__ __forceinline__ uint32_t half(const uint32_t *a, int i)
-{
-    return (i & 1) ? (a[i >> 1] >> 16) : (a[i >> 1] & 0xffffu);
-}
-
-/* a ^ b ^ c in one VALU op (gfx950 v_bitop3_b32, truth table 0x96) */
-__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c)
-{
-    return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
-}
-
-/* Maximum of v (< 64) over the ACTIVE lanes of the wave, bit by bit from
- * ballots.  (A shuffle butterfly is wrong here: lanes that have left the
- * codeword's control flow do not forward partial maxima.) */
-__device__ __forceinline__ uint32_t wave_max(uint32_t v)
-{
-    uint32_t m = 0;
-#pragma unroll
-    for (int b = 5; b >= 0; --b) {
-        const uint32_t c = m | (1u << b);
-        if (__ballot(v >= c) != 0ull)
-            m = c;
-    }
-    return m;
-}
-
-__device__ __forceinline__ uint32_t wave_min(uint32_t v) { return 63u - wave_max(63u - v); }
-
-/* Maximum of v over all 64 lanes -- only where every lane of the wave is
- * active (the BM loop: the kernel enters the correction with the whole wave).
- * DPP row shifts give each row's inclusive maximum in its lane 15, two row
- * broadcasts fold the rows into lane 63. */
-__device__ __forceinline__ uint32_t wave_max_full(uint32_t v)
-{
-    uint32_t x = v;
-    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, true)); /* row_shr:1 */
-    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, true)); /* row_shr:2 */
-    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, true)); /* row_shr:4 */
-    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, true)); /* row_shr:8 */
-    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xa, 0xf, false)); /* row_bcast:15 */
-    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false)); /* row_bcast:31 */
-    return __builtin_amdgcn_readlane(x, 63);
-}
-
-/* byte-wise zero test of 16 bytes -> 16-bit mask (bit b: byte b is zero) */
-__device__ __forceinline__ uint32_t zero_bytes16(const uint32_t (&v)[4])
-{
-    uint32_t m = 0;
-#pragma unroll
-    for (int d = 0; d < 4; ++d) {
-        const uint32_t z = ~(((v[d] & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | v[d] | 0x7F7F7F7Fu); /* bit 8b+7 */
-        const uint32_t t = (z >> 7) & 0x01010101u;
-        m |= ((t * 0x10204080u) >> 28) << (4 * d);
-    }
-    return m;
-}
-
-/* Walks a 256-bit root map over i' = i mod 255 in the reference's order:
- * i = 1..254 ascending, then i = 255 (bit 0).  No per-lane loops. */
-struct RootIter {
-    uint32_t w[9]; /* w[0..7]: bits of i' (bit 0 of w[0] removed), w[8]: the i = 255 bit */
-    __device__ __forceinline__ void init(const uint32_t (&rb)[8])
-    {
-#pragma unroll
-        for (int k = 0; k < 8; ++k)
-            w[k] = rb[k];
-        w[8] = rb[0] & 1u;
-        w[0] &= ~1u;
-    }
-    __device__ __forceinline__ uint32_t next()
-    {
-        uint32_t sel = 8, bits = w[8];
-#pragma unroll
-        for (int k = 7; k >= 0; --k) {
-            const bool nz = w[k] != 0u;
-            sel = nz ? (uint32_t)k : sel;
-            bits = nz ? w[k] : bits;
-        }
-        const uint32_t b = __builtin_ctz(bits | 0x80000000u);
-        const uint32_t clr = bits & (bits - 1u);
-#pragma unroll
-        for (int k = 0; k < 9; ++k)
-            w[k] = (sel == (uint32_t)k) ? clr : w[k];
-        return sel < 8u ? 32u * sel + b : 255u;
-    }
+    /* "address-form" logs (BM): a = 128 log v + pa, zero = 0xFFFF + pa: the
+     * exp byte of a plus a scaled log s is at LDS byte a + s */
+    __device__ __forceinline__ uint32_t expa(uint32_t a) const { return lds8(a); }
+    /* the base of address-form logs */
+    __device__ __forceinline__ uint32_t pofs() const { return pa; }
 };
 
 template <typename PosT, bool ERA>
@@ -755,8 +653,16 @@ __global__ __launch_bounds__(COR_WG) void rs_correct_k(const RsDevTables *__rest
                                                        const uint16_t *__restrict__ syn16, size_t syn16_stride,
                                                        const PosT *__restrict__ pos, size_t pos_stride,
                                                        const uint8_t *__restrict__ cnt, uint8_t *__restrict__ ok,
-                                                       uint8_t *__restrict__ corrected)
+                                                       uint8_t *__restrict__ corrected,
+                                                       const uint32_t *__restrict__ list,
+                                                       const uint32_t *__restrict__ list_n)
 {
+    /* list mode (the split decode's fallback, rs_fast.hip): the codewords
+     * list[0 .. *list_n); otherwise 0 .. count - 1.  Blocks with no work
+     * leave before filling the tables. */
+    const size_t n = list ? (size_t)*list_n : count;
+    if ((size_t)blockIdx.x * COR_WG >= n)
+        return;
     /* one block, carved by hand: the layout (and lgf ending exactly at the
      * allocation's end) is part of the arithmetic, see the header */
     __shared__ uint4 lds[LDS_END / 16];
@@ -772,16 +678,17 @@ __global__ __launch_bounds__(COR_WG) void rs_correct_k(const RsDevTables *__rest
     for (uint32_t t = threadIdx.x; t < 16u * 256u; t += COR_WG)
         lch[t] = T->chien[t];
     __syncthreads();
-    const Gf gf{reinterpret_cast<const uint8_t *>(lgf) + (threadIdx.x & (GF_REPL - 1)) * 4 + 1};
+    const Gf gf{lds_addr(lgf) + (threadIdx.x & (GF_REPL - 1)) * 4 + 1};
     uint8_t *srow = lsyn + threadIdx.x;
 
     /* The trip count is uniform per workgroup and the whole wave enters the
      * correction when any of its codewords needs it (the rest, with zero
      * syndromes, ride through BM as no-ops and leave at deg = 0): the BM
      * bounds are then full-wave DPP reductions. */
-    for (size_t base = (size_t)blockIdx.x * COR_WG; base < count; base += (size_t)gridDim.x * COR_WG) {
-        const size_t cw = base + threadIdx.x;
-        const bool valid = cw < count;
+    for (size_t base = (size_t)blockIdx.x * COR_WG; base < n; base += (size_t)gridDim.x * COR_WG) {
+        const size_t idx = base + threadIdx.x;
+        const bool valid = idx < n;
+        const size_t cw = list ? (valid ? (size_t)list[idx] : 0) : idx;
         uint32_t sw[8] = {0, 0, 0, 0, 0, 0, 0, 0};
         bool ext_bad = false; /* external syndrome > 255: out-of-table in the reference, refused */
         if (valid && syn16) {
@@ -844,12 +751,29 @@ extern "C" hipError_t rsk_correct(const RsDevTables *tab, const RsCorrParams *pr
     const dim3 grid(persistent_grid(count, COR_WG, num_cu));
     if (pos32)
         hipLaunchKernelGGL((rs_correct_k<uint32_t, true>), grid, dim3(COR_WG), 0, stream, tab, *prm, data, dstride,
-                           parity, pstride, count, syn, syn16, syn16_stride, pos32, pos_stride, cnt, ok, corrected);
+                           parity, pstride, count, syn, syn16, syn16_stride, pos32, pos_stride, cnt, ok, corrected, nullptr, nullptr);
     else if (pos8)
         hipLaunchKernelGGL((rs_correct_k<uint8_t, true>), grid, dim3(COR_WG), 0, stream, tab, *prm, data, dstride,
-                           parity, pstride, count, syn, syn16, syn16_stride, pos8, pos_stride, cnt, ok, corrected);
+                           parity, pstride, count, syn, syn16, syn16_stride, pos8, pos_stride, cnt, ok, corrected, nullptr, nullptr);
     else /* error mode */
         hipLaunchKernelGGL((rs_correct_k<uint8_t, false>), grid, dim3(COR_WG), 0, stream, tab, *prm, data, dstride,
-                           parity, pstride, count, syn, syn16, syn16_stride, pos8, pos_stride, cnt, ok, corrected);
+                           parity, pstride, count, syn, syn16, syn16_stride, pos8, pos_stride, cnt, ok, corrected, nullptr, nullptr);
+    return hipGetLastError();
+}
+
+/* error-mode correction of the codewords list[0 .. *list_n) (the count is read
+ * on the device: the split decode's fallback, rs_fast.hip) */
+extern "C" hipError_t rsk_correct_list(const RsDevTables *tab, const RsCorrParams *prm, uint8_t *data, size_t dstride,
+                                       uint8_t *parity, size_t pstride, size_t count, const uint8_t *syn,
+                                       const uint32_t *list, const uint32_t *list_n, uint8_t *ok,
+                                       uint8_t *corrected, int num_cu, hipStream_t stream)
+{
+    if (count == 0)
+        return hipSuccess;
+    /* the list is empty for codewords with at most 16 errors: a small grid
+     * leaves quickly (each block loops over the list when it is long) */
+    const dim3 grid(std::min(persistent_grid(count, COR_WG, num_cu), 64));
+    hipLaunchKernelGGL((rs_correct_k<uint8_t, false>), grid, dim3(COR_WG), 0, stream, tab, *prm, data, dstride,
+                       parity, pstride, count, syn, nullptr, 0, nullptr, 0, nullptr, ok, corrected, list, list_n);
     return hipGetLastError();
 }

@@ -59,10 +59,52 @@ struct RsCorrParams {
     uint32_t vfast;  /* (fcr+31)*prim*254 < 32768: verification exponents need no int16 emulation */
     uint32_t force_verify; /* run the re-syndrome check even where it provably passes (tests) */
     uint32_t stop_at;      /* profiling only (stage ablation): 0 = full decode; 1/2/3/4 = return
-                              after syndrome load / erasure+BM / Omega / Chien (results invalid) */
+                              after syndrome load / erasure+BM / Omega / Chien (results invalid);
+                              5 = split decode without the apply */
     uint8_t tr_start[RS_NR];
     uint8_t tr_inc[RS_NR];
 };
+
+/*
+ * Workspace of the split error-mode decode (rs_fast.hip), carved from one
+ * device buffer for `cap` codewords (every array 16-byte aligned):
+ *   syn   32 B  poly-form syndromes (rsk_syndrome)
+ *   lam   16 B  log Lambda_1..16 (255 = zero)            (rsk_bm)
+ *   om    16 B  log Omega_0..15 (255 = zero)             (rsk_bm)
+ *   roots 32 B  root map over the points alpha^i', i' = 0..255 (rsk_chien),
+ *               then the corrections: 16 locations, 16 magnitudes (rsk_forney)
+ *   meta   1 B  state << 5 | deg(Lambda)                 (rsk_bm, rsk_chien)
+ *   list   4 B  codewords handed to the general kernel (rsk_correct_list)
+ *   nlist  the list's length (zeroed by rsk_syndrome)
+ */
+#define RS_ST_DONE 0u /* ok / corrected written */
+#define RS_ST_FAST 1u /* deg(Lambda) = L <= 16: Chien, then Forney */
+#define RS_ST_LIST 2u /* on the list: the general kernel decodes it */
+
+struct RsSplitWs {
+    uint8_t *syn, *lam, *om, *roots, *meta;
+    uint32_t *list, *nlist;
+};
+
+static inline size_t rs_ws_round16(size_t n) { return (n + 15) & ~(size_t)15; }
+
+static inline size_t rs_ws_bytes(size_t cap)
+{
+    return 96 * cap + rs_ws_round16(cap) + rs_ws_round16(4 * cap) + 16;
+}
+
+static inline RsSplitWs rs_ws_carve(uint8_t *base, size_t cap)
+{
+    RsSplitWs w;
+    w.syn = base;
+    w.lam = w.syn + 32 * cap;
+    w.om = w.lam + 16 * cap;
+    w.roots = w.om + 16 * cap;
+    w.meta = w.roots + 32 * cap;
+    w.list = (uint32_t *)(w.meta + rs_ws_round16(cap));
+    w.nlist = (uint32_t *)((uint8_t *)w.list + rs_ws_round16(4 * cap));
+    return w;
+}
 
 #ifdef __cplusplus
 extern "C" {
@@ -76,6 +118,11 @@ hipError_t rsk_encode(const RsDevTables *tab, const uint8_t *data, size_t dstrid
  * remainder of (data || parity) * x^32 mod g and the synt transform */
 hipError_t rsk_syndrome(const RsDevTables *tab, const uint8_t *data, size_t dstride, const uint8_t *parity,
                         size_t pstride, uint32_t size, size_t count, uint8_t *syn, int num_cu, hipStream_t stream);
+/* the same, also zeroing *reset before any later launch on the stream runs
+ * (the split decode's list length) */
+hipError_t rsk_syndrome_reset(const RsDevTables *tab, const uint8_t *data, size_t dstride, const uint8_t *parity,
+                              size_t pstride, uint32_t size, size_t count, uint8_t *syn, uint32_t *reset, int num_cu,
+                              hipStream_t stream);
 
 /* poly syndromes (32 B per codeword, rsk_syndrome) -> log form: out[c*stride + i]
  * = log S_i (255 = zero), flag[c] = any S_i nonzero; out / flag may be NULL */
@@ -99,6 +146,31 @@ hipError_t rsk_correct(const RsDevTables *tab, const RsCorrParams *prm, uint8_t 
                        const uint8_t *pos8,
                        const uint32_t *pos32, size_t pos_stride, const uint8_t *cnt, uint8_t *ok, uint8_t *corrected,
                        int num_cu, hipStream_t stream);
+
+/* error-mode correction of the codewords list[0 .. *list_n) (count bounds the
+ * grid; the length is read on the device) */
+hipError_t rsk_correct_list(const RsDevTables *tab, const RsCorrParams *prm, uint8_t *data, size_t dstride,
+                            uint8_t *parity, size_t pstride, size_t count, const uint8_t *syn, const uint32_t *list,
+                            const uint32_t *list_n, uint8_t *ok, uint8_t *corrected, int num_cu, hipStream_t stream);
+
+/*
+ * Split error-mode decode (rs_fast.hip), after rsk_syndrome_reset into ws.syn:
+ *   rsk_bm     Berlekamp-Massey + Omega -> ws.lam / ws.om / ws.meta; clean
+ *              codewords finished; deg != L or L > 16 -> ws.list
+ *   rsk_chien  root map -> ws.roots; root count != deg finished (failure)
+ *   rsk_forney magnitudes -> ws.roots (as correction records), ok / corrected
+ *   rsk_apply  the corrections into the codewords
+ * then rsk_correct_list over ws.list.  Needs RsCorrParams.vfast.
+ */
+hipError_t rsk_bm(const RsDevTables *tab, const RsSplitWs *ws, size_t count, uint8_t *ok, uint8_t *corrected,
+                  int num_cu, hipStream_t stream);
+hipError_t rsk_chien(const RsDevTables *tab, const RsCorrParams *prm, const RsSplitWs *ws, size_t count, uint8_t *ok,
+                     uint8_t *corrected, int num_cu, hipStream_t stream);
+hipError_t rsk_forney(const RsDevTables *tab, const RsCorrParams *prm, const RsSplitWs *ws, uint8_t *data,
+                      size_t dstride, uint8_t *parity, size_t pstride, size_t count, uint8_t *ok, uint8_t *corrected,
+                      int num_cu, hipStream_t stream);
+hipError_t rsk_apply(const RsCorrParams *prm, const RsSplitWs *ws, uint8_t *data, size_t dstride, uint8_t *parity,
+                     size_t pstride, size_t count, hipStream_t stream);
 
 #ifdef __cplusplus
 }

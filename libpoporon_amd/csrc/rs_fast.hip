@@ -1,0 +1,709 @@
+/*
+ * rs_fast.hip -- RS(255,223) error-mode decode split into three kernels,
+ * each small enough in LDS (<= 64 KiB) and registers (<= 64 VGPRs) for two
+ * 1024-thread workgroups per CU: 8 waves per SIMD, twice the occupancy of
+ * the single correction kernel (rs_correct.hip, 160 KiB + 128 VGPRs), whose
+ * time was half waiting on LDS results.  One codeword per lane.
+ *
+ *   rs_bm_k      syndromes -> Berlekamp-Massey (src/decode.c:49-96) -> Lambda,
+ *                degree (:98-110), Omega (:147-158)
+ *   rs_chien_k   Lambda -> root map over the 255 points (:112-145)
+ *   rs_forney_k  roots, Omega, Lambda -> Forney magnitudes (:159-191), apply
+ *                (:215-226)
+ *
+ * Fast path = the codewords the reference corrects without its re-syndrome
+ * check being able to fail: deg(Lambda) = L <= 16 (then Lambda has deg
+ * distinct roots or the root count check fails, and Forney's magnitudes
+ * reproduce every syndrome -- rs_correct.hip header).  Everything else --
+ * L > 16, a locator that would grow past x^16, deg != L, deg = 0 -- is put
+ * on a list that the general kernel (rs_correct_k, list mode) decodes with
+ * the reference's full-length arrays and checks.  Results are bit-exact
+ * either way; the list is empty for codewords with at most 16 errors.
+ *
+ * GF table of rs_bm_k / rs_forney_k (64 KiB; dword x * 32 + r, x < 512,
+ * replica r = lane & 31 so every lane's byte reads hit bank lane & 31):
+ *   byte 0     0
+ *   byte 1     exp2[x]
+ *   bytes 2-3  for x < 256: the "address-form" log of x, 128 log x + 4r + 1
+ *              (the LDS address of this replica's exp byte of log x), and
+ *              for x = 0 the zero AZ = 128 Z0 + 4r (a byte 0); 0 for x >= 256
+ * exp of an address-form log a plus a plain scaled log s = 128 log is the
+ * byte at a + s.  Zeros never leave the table: the plain scaled zero is
+ * SZ = 128 Z0 - 1 (= log of 0 as returned by the table minus 4r + 1), and
+ * with Z0 = 200 every sum with a zero operand lands on a byte 0 (AZ + s,
+ * a + SZ) or on a high log byte of an entry >= 256 (AZ + SZ), all zero.
+ * (Past a 64 KiB allocation a read is not reliably 0: the first bytes after
+ * it return another workgroup's LDS, tools/probes/lds_oob64.hip.)  Valid
+ * address-form logs are odd, zeros even.
+ *
+ * Chien table of rs_chien_k (65,280 B, the whole allocation): the 16-byte
+ * row of term j (1..16) at 16 consecutive points, alpha^(e + j b) for
+ * b = 0..15, stored at e * 256 + (j - 1) * 16.  Lane l visits the terms in
+ * the order j = ((k + l) mod 16) + 1, k = 0..15, so the 16 lanes of every
+ * ds_read_b128 lane group read 16 different bank slots: conflict-free
+ * whatever the coefficients (the single kernel's data-dependent rows cost
+ * 32 M conflict cycles per 2^20 codewords, profiles/r01_pmc_stages_v10.txt).
+ */
+#include <hip/hip_runtime.h>
+
+#include <type_traits>
+
+#include "rs_device.h"
+#include "rs_lane.h"
+
+#define FWG 1024       /* threads per workgroup; two workgroups per CU */
+#define NL 17          /* Lambda_0..16 and B_0..16: t = 16 */
+#define Z0 200u        /* zero sentinels: AZ = 128 Z0 + 4r, SZ = 128 Z0 - 1 (see the header) */
+#define SZ (128u * Z0 - 1u)
+#ifndef FORNEY_R
+#define FORNEY_R 1     /* roots per Forney step (more spill at 64 VGPRs) */
+#endif
+#ifndef FORNEY_WAVES
+#define FORNEY_WAVES 8
+#endif
+#ifndef BM_WAVES
+#define BM_WAVES 8
+#endif
+
+/* ------------------------------------------------------------------------ */
+/* GF table (rs_bm_k, rs_forney_k)                                          */
+/* ------------------------------------------------------------------------ */
+
+__device__ __forceinline__ void fill_gfa(uint32_t *lgf, const RsDevTables *__restrict__ T)
+{
+    for (uint32_t t = threadIdx.x; t < 512u * 32u; t += FWG) {
+        const uint32_t x = t >> 5, r = t & 31u;
+        const uint32_t la = x < 256u ? (x ? (uint32_t)T->log[x] * 128u + 4u * r + 1u : 128u * Z0 + 4u * r) : 0u;
+        lgf[t] = ((uint32_t)T->exp2[x] << 8) | (la << 16);
+    }
+}
+
+struct GfA {
+    uint32_t pofs; /* 4 (lane & 31) + 1: this replica's exp byte of log 0 */
+    /* this replica's address-form zero */
+    __device__ __forceinline__ uint32_t az() const { return pofs + SZ; }
+    /* exp of an address-form log plus a plain scaled log */
+    __device__ __forceinline__ uint32_t expa(uint32_t a) const { return lds8(a); }
+    /* address-form log of v < 256 (AZ for 0) */
+    __device__ __forceinline__ uint32_t loga(uint32_t v) const { return lds16(pofs + 1u + (v << 7)); }
+    /* plain scaled log 128 log v (SZ for 0) */
+    __device__ __forceinline__ uint32_t logs(uint32_t v) const { return loga(v) - pofs; }
+    /* log (0..254) of an address-form log, 255 for zero */
+    __device__ __forceinline__ uint32_t plog(uint32_t a) const { return (a & 1u) ? (a - pofs) >> 7 : 255u; }
+    /* address-form log of a stored byte log (255 = zero) */
+    __device__ __forceinline__ uint32_t afrom(uint32_t b) const { return b < 255u ? (b << 7) + pofs : az(); }
+    /* alpha^l of a plain log l < 255 */
+    __device__ __forceinline__ uint32_t exp(uint32_t l) const { return lds8(pofs + (l << 7)); }
+};
+
+static int fast_grid(size_t count, int num_cu)
+{
+    const size_t need = (count + FWG - 1) / FWG;
+    const size_t g = 2u * (size_t)(num_cu > 0 ? num_cu : 256);
+    return (int)(need < g ? (need ? need : 1) : g);
+}
+
+/* ------------------------------------------------------------------------ */
+/* rs_bm_k: Berlekamp-Massey + Omega                                         */
+/* ------------------------------------------------------------------------ */
+
+/*
+ * BM in Massey's unnormalised form over address-form logs, as rs_correct.hip
+ * (which shows every product equal to the reference's Karn form), with the
+ * arrays cut to 17 coefficients.  The cut is exact while L <= 16 and
+ * B_16..B_32 play no part: an update with B_16 != 0 (or with B's part past
+ * x^16 nonzero, `bo`) would give Lambda a term past x^16, and lengthening
+ * to L > 16 ends with deg != L -- all of these go to the list.
+ *
+ * Syndromes enter a window of 20 u16 entries (10 VGPRs), four per block of
+ * four iterations: at block q the entry e holds 128 log S_(4q+3-e), so term
+ * i of iteration r = 4q+1+s reads entry 3 - s + i at a compile-time place
+ * (the four iterations are unrolled; blocks are a rolled loop).
+ */
+__global__ __launch_bounds__(FWG, BM_WAVES) void rs_bm_k(const RsDevTables *__restrict__ T, const uint8_t *__restrict__ syn,
+                                                   size_t count, uint8_t *__restrict__ lamo, uint8_t *__restrict__ omo,
+                                                   uint8_t *__restrict__ meta, uint32_t *__restrict__ list,
+                                                   uint32_t *__restrict__ nlist, uint8_t *__restrict__ ok,
+                                                   uint8_t *__restrict__ corrected)
+{
+    __shared__ uint32_t lgf[512 * 32];
+    fill_gfa(lgf, T);
+    __syncthreads();
+    const GfA gf{lds_addr(lgf) + 4u * (threadIdx.x & 31u) + 1u};
+    const uint32_t pofs = gf.pofs;
+    const uint32_t AZ = gf.az();         /* address-form zero */
+    constexpr uint32_t DQZ = SZ;         /* "no update": dq + B's logs read zeros */
+
+    for (size_t base = (size_t)blockIdx.x * FWG; base < count; base += (size_t)gridDim.x * FWG) {
+        const size_t cw = base + threadIdx.x;
+        const bool valid = cw < count;
+        const uint32_t *sp = reinterpret_cast<const uint32_t *>(syn + (valid ? cw : 0) * RS_NR);
+        uint4 sa = make_uint4(0, 0, 0, 0), sb = sa;
+        if (valid) {
+            sa = reinterpret_cast<const uint4 *>(sp)[0];
+            sb = reinterpret_cast<const uint4 *>(sp)[1];
+        }
+        const bool any = (sa.x | sa.y | sa.z | sa.w | sb.x | sb.y | sb.z | sb.w) != 0u;
+        if (__ballot(any) == 0ull) { /* uniform: every codeword of the wave is clean */
+            if (valid) {
+                ok[cw] = 1;
+                if (corrected)
+                    corrected[cw] = 0;
+                meta[cw] = (uint8_t)(RS_ST_DONE << 5);
+            }
+            continue;
+        }
+
+        /* ---- Berlekamp-Massey, src/decode.c:49-96 (error mode: r = 1..32) ---- */
+        /* al: address-form logs of Lambda_0..16 (Lambda_0 = 1, never updated);
+         * BP: B_0..B_17 the same way, packed two per register (B_17 stays zero) */
+        uint32_t al[NL], BP[(NL + 1) / 2];
+        al[0] = pofs;
+#pragma unroll
+        for (int i = 1; i < NL; ++i)
+            al[i] = AZ;
+        BP[0] = pofs | (AZ << 16);
+#pragma unroll
+        for (int k = 1; k < (NL + 1) / 2; ++k)
+            BP[k] = AZ | (AZ << 16);
+        uint32_t dl = 0, db = 0, L = 0, lb = 0, ubp = 0;
+        bool over = false, bo = false;
+        uint32_t WL[10];
+#pragma unroll
+        for (int k = 0; k < 10; ++k)
+            WL[k] = SZ | (SZ << 16);
+        uint32_t snext = any ? sa.x : 0u; /* S_0..S_3 */
+
+        auto step = [&](auto sc, uint32_t r) __attribute__((always_inline)) {
+            constexpr int s = decltype(sc)::value;
+            const uint32_t ub = ubp; /* dl <= the previous iteration's bound */
+            uint32_t disc = 0;
+#pragma unroll
+            for (int g = 0; g < NL; g += 8) {
+                if ((uint32_t)g <= ub) {
+#pragma unroll
+                    for (int i = g; i < g + 8 && i < NL; ++i)
+                        disc ^= gf.expa(al[i] + half(WL, 3 - s + i)); /* S_(r-1-i), zero where r-1-i < 0 */
+                }
+            }
+            const uint32_t ld = gf.logs(disc);
+            const bool upd = disc != 0u;
+            const bool lengthen = upd && (2u * L <= r - 1u);
+            const int32_t dd = (int32_t)ld - (int32_t)lb;
+            const uint32_t dq = upd ? (uint32_t)(dd < 0 ? dd + 255 * 128 : dd) : DQZ; /* scaled log of disc / b */
+            const bool b16 = half(BP, NL - 1) != AZ;
+            over = over || (upd && (bo || b16)); /* Lambda would get a term past x^16 */
+            bo = lengthen ? false : (bo || b16);  /* B <- x B pushes B_16 past the cut */
+            const uint32_t up = min((uint32_t)(NL - 1), max(dl, db + 1u));
+            const uint32_t ub2 = wave_max_full(up);
+            ubp = ub2;
+            /* groups of four coefficients 4m..4m+3 (two B pairs), top down:
+             * Lambda_i += q B_(i-1); B <- Lambda (old) or x B, pair k from the
+             * old pairs k and k-1 */
+#pragma unroll
+            for (int m = (NL - 1) / 4; m >= 0; --m) {
+                if ((uint32_t)(4 * m) <= ub2) {
+                    uint32_t old[4];
+#pragma unroll
+                    for (int i = 4 * m + 3; i >= 4 * m; --i) {
+                        if (i >= NL)
+                            continue;
+                        old[i - 4 * m] = al[i];
+                        if (i > 0) {
+                            const uint32_t v = gf.expa(al[i]) ^ gf.expa(dq + half(BP, i - 1));
+                            al[i] = gf.loga(v);
+                        }
+                    }
+#pragma unroll
+                    for (int k = 2 * m + 1; k >= 2 * m; --k) {
+                        if (k >= (NL + 1) / 2)
+                            continue;
+                        const uint32_t lo = old[2 * k - 4 * m];
+                        const uint32_t hi = 2 * k + 1 < NL ? old[2 * k + 1 - 4 * m] : AZ;
+                        const uint32_t sh = k > 0 ? __builtin_amdgcn_alignbyte(BP[k], BP[k - 1], 2)
+                                                  : ((BP[0] << 16) | AZ);
+                        BP[k] = lengthen ? (lo | (hi << 16)) : sh;
+                    }
+                }
+            }
+            db = lengthen ? dl : min(db + 1u, (uint32_t)(NL - 1));
+            if (upd)
+                dl = up;
+            if (lengthen) {
+                L = r - L;
+                lb = ld;
+            }
+        };
+#pragma unroll 1
+        for (uint32_t q = 0; q < RS_NR / 4; ++q) {
+            const uint32_t sd = snext;
+            if (q + 1u < RS_NR / 4) /* uniform */
+                snext = any ? sp[q + 1u] : 0u;
+            /* shift the window by four entries, S_(4q+3) .. S_(4q) in front */
+#pragma unroll
+            for (int k = 9; k >= 2; --k)
+                WL[k] = WL[k - 2];
+            const uint32_t s0 = gf.logs(sd & 0xffu), s1 = gf.logs((sd >> 8) & 0xffu);
+            const uint32_t s2 = gf.logs((sd >> 16) & 0xffu), s3 = gf.logs(sd >> 24);
+            WL[0] = s3 | (s2 << 16);
+            WL[1] = s1 | (s0 << 16);
+            step(std::integral_constant<int, 0>{}, 4u * q + 1u);
+            step(std::integral_constant<int, 1>{}, 4u * q + 2u);
+            step(std::integral_constant<int, 2>{}, 4u * q + 3u);
+            step(std::integral_constant<int, 3>{}, 4u * q + 4u);
+        }
+
+        /* ---- degree, src/decode.c:98-110 ---- */
+        uint32_t deg = 0;
+#pragma unroll
+        for (int i = 0; i < NL; ++i)
+            deg = (al[i] & 1u) ? (uint32_t)i : deg;
+        const bool fast = any && !over && deg == L && deg != 0u;
+
+        /* ---- Omega = S * Lambda mod x^deg (log form), src/decode.c:147-158 ---- */
+        uint32_t ob[4] = {0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
+        const uint32_t degmax = wave_max(fast ? deg : 0u);
+        if (degmax) {
+            /* S_0..S_15 again (L2): keeping them live through BM costs registers */
+            const uint4 s4 = any ? reinterpret_cast<const uint4 *>(sp)[0] : make_uint4(0, 0, 0, 0);
+            const uint32_t sw[4] = {s4.x, s4.y, s4.z, s4.w};
+            auto omega = [&](auto dmc) __attribute__((always_inline)) {
+                constexpr int DM = decltype(dmc)::value; /* > 0: every lane's bound is DM (no guards) */
+                uint32_t sl[8]; /* plain scaled logs of S_0..S_15, two per register */
+#pragma unroll
+                for (int k = 0; k < 16; k += 2)
+                    sl[k >> 1] = gf.logs((sw[k >> 2] >> (8 * (k & 3))) & 0xffu) |
+                                 (gf.logs((sw[k >> 2] >> (8 * ((k + 1) & 3))) & 0xffu) << 16);
+#pragma unroll
+                for (int m = 0; m < 16; ++m) {
+                    if (DM ? m < DM : (uint32_t)m < degmax) {
+                        uint32_t acc = 0;
+#pragma unroll
+                        for (int j = 0; j <= m; ++j)
+                            acc ^= gf.expa(al[j] + half(sl, m - j));
+                        const uint32_t o = (uint32_t)m < deg ? gf.plog(gf.loga(acc)) : 255u;
+                        ob[m >> 2] ^= (o ^ 0xffu) << (8 * (m & 3));
+                    }
+                    __builtin_amdgcn_sched_barrier(0); /* one coefficient's lookups at a time: registers */
+                }
+            };
+            if (degmax == 16u)
+                omega(std::integral_constant<int, 16>{});
+            else
+                omega(std::integral_constant<int, 0>{});
+        }
+
+        if (valid) {
+            if (!any) {
+                ok[cw] = 1;
+                if (corrected)
+                    corrected[cw] = 0;
+                meta[cw] = (uint8_t)(RS_ST_DONE << 5);
+            } else if (!fast) {
+                meta[cw] = (uint8_t)(RS_ST_LIST << 5);
+                list[atomicAdd(nlist, 1u)] = (uint32_t)cw;
+            } else {
+                uint32_t lb4[4] = {0, 0, 0, 0};
+#pragma unroll
+                for (int j = 1; j < NL; ++j)
+                    lb4[(j - 1) >> 2] |= gf.plog(al[j]) << (8 * ((j - 1) & 3));
+                reinterpret_cast<uint4 *>(lamo)[cw] = make_uint4(lb4[0], lb4[1], lb4[2], lb4[3]);
+                reinterpret_cast<uint4 *>(omo)[cw] = make_uint4(ob[0], ob[1], ob[2], ob[3]);
+                meta[cw] = (uint8_t)((RS_ST_FAST << 5) | deg);
+            }
+        }
+    }
+}
+
+/* ------------------------------------------------------------------------ */
+/* rs_chien_k: root map                                                      */
+/* ------------------------------------------------------------------------ */
+
+/*
+ * Lambda(alpha^i'), i' = 16a + b, is 1 + sum_j row_j[e_j(a)]_b with
+ * e_j(a) = (log Lambda_j + 16 a j) mod 255: 16 ds_read_b128 per 16 points.
+ * Slot k of lane l holds term j_k = ((k + l) mod 16) + 1 as the LDS address
+ * of its row, e * 256 + (j_k - 1) * 16, stepped by (16 j_k mod 255) * 256
+ * per chunk and reduced below 255 * 256 by min(t, t - 255 * 256); a zero
+ * coefficient points at the all-zero rows e = 255 and steps by 255 * 256,
+ * which the reduction maps back onto itself (no read leaves the table).
+ */
+__global__ __launch_bounds__(FWG, 8) void rs_chien_k(const RsDevTables *__restrict__ T, RsCorrParams P, size_t count,
+                                                      const uint8_t *__restrict__ lam, uint8_t *__restrict__ meta,
+                                                      uint8_t *__restrict__ roots, uint8_t *__restrict__ ok,
+                                                      uint8_t *__restrict__ corrected)
+{
+    __shared__ uint4 lch[256 * 16];
+    for (uint32_t t = threadIdx.x; t < 256u * 16u; t += FWG)
+        lch[t] = T->chien[(t & 15u) * 256u + (t >> 4)];
+    __syncthreads();
+    const uint32_t cb = lds_addr(lch);
+    const uint32_t lr0 = threadIdx.x & 15u;
+    constexpr uint32_t WRAP = 255u * 256u;
+
+    for (size_t base = (size_t)blockIdx.x * FWG; base < count; base += (size_t)gridDim.x * FWG) {
+        const size_t cw = base + threadIdx.x;
+        const bool valid = cw < count;
+        const uint32_t st = valid ? meta[cw] : 0u;
+        const bool fast = (st >> 5) == RS_ST_FAST;
+        if (__ballot(fast) == 0ull)
+            continue;
+        const uint32_t deg = fast ? (st & 31u) : 0u;
+        uint4 l4 = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu);
+        if (fast)
+            l4 = reinterpret_cast<const uint4 *>(lam)[cw];
+        /* rotate the 16 log bytes by lr: byte k of R = log Lambda_(j_k) (lr
+         * made opaque per codeword: hoisted, its 32 derived constants spill) */
+        uint32_t lr = lr0;
+        asm volatile("" : "+v"(lr));
+        uint32_t D[4] = {l4.x, l4.y, l4.z, l4.w};
+        uint32_t E[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            E[k] = (lr & 4u) ? D[(k + 1) & 3] : D[k];
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            D[k] = (lr & 8u) ? E[(k + 2) & 3] : E[k];
+        uint32_t R[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            R[k] = __builtin_amdgcn_alignbyte(D[(k + 1) & 3], D[k], lr & 3u);
+        uint32_t A[16], inc[16];
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            const uint32_t jm = ((uint32_t)k + lr) & 15u; /* j_k - 1 */
+            const uint32_t e = (R[k >> 2] >> (8 * (k & 3))) & 0xffu;
+            A[k] = cb + (e << 8) + (jm << 4);
+            inc[k] = e == 255u ? WRAP : (jm == 15u ? 256u : (jm + 1u) << 12);
+        }
+        /* the map's words go to memory as they come (registers are short);
+         * the pad check below reads them back */
+        uint32_t *rmap = reinterpret_cast<uint32_t *>(roots + (valid ? cw : 0) * 32u);
+        uint32_t cnt = 0;
+#pragma unroll 1
+        for (int w = 0; w < 8; ++w) {
+            uint32_t word = 0;
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                uint32_t acc[4] = {0x01010101u, 0x01010101u, 0x01010101u, 0x01010101u};
+#pragma unroll
+                for (int k = 0; k < 16; k += 2) {
+                    const lds_u32x4_t r1 = lds128(A[k]), r2 = lds128(A[k + 1]);
+                    const uint32_t t1 = A[k] + inc[k], t2 = A[k + 1] + inc[k + 1];
+                    A[k] = min(t1, t1 - WRAP);
+                    A[k + 1] = min(t2, t2 - WRAP);
+                    acc[0] = xor3(acc[0], r1.x, r2.x);
+                    acc[1] = xor3(acc[1], r1.y, r2.y);
+                    acc[2] = xor3(acc[2], r1.z, r2.z);
+                    acc[3] = xor3(acc[3], r1.w, r2.w);
+                }
+                word |= zero_bytes16(acc) << (16 * h);
+            }
+            if (w == 7)
+                word &= 0x7FFFFFFFu; /* i' = 255 repeats i' = 0 */
+            cnt += __popc(word);
+            if (fast)
+                rmap[w] = word;
+        }
+        bool good = cnt == deg; /* src/decode.c:143-145 */
+        if (P.pad > 0) {
+            /* locations k = (i iprim - 1) mod 255 below pad fail, src/decode.c:132-134 */
+            uint32_t rb[8];
+#pragma unroll
+            for (int w = 0; w < 8; ++w)
+                rb[w] = fast ? rmap[w] : 0u;
+            RootIter it;
+            it.init(rb);
+            bool low = false;
+            const uint32_t cmax = wave_max(good ? cnt : 0u);
+            for (uint32_t n = 0; n < cmax; ++n) {
+                const uint32_t i = it.next();
+                low |= n < cnt && (int32_t)((i * P.iprim + 254u) % 255u) < P.pad;
+            }
+            good = good && !low;
+        }
+        if (fast && !good) {
+            {
+                ok[cw] = 0;
+                if (corrected)
+                    corrected[cw] = 0;
+                meta[cw] = (uint8_t)(RS_ST_DONE << 5);
+            }
+        }
+    }
+}
+
+/* ------------------------------------------------------------------------ */
+/* rs_forney_k: magnitudes and apply                                         */
+/* ------------------------------------------------------------------------ */
+
+/*
+ * Per root i (ascending, src/decode.c:136-138): num = sum_m Omega_m
+ * alpha^(i m), den = sum_(2h <= dtop) Lambda_(2h+1) alpha^(2h i), magnitude
+ * alpha^(log num + log alpha^(i (fcr-1)) + 255 - log den) (no den = 0 guard,
+ * as the reference); a zero numerator corrects nothing and is not counted.
+ * FORNEY_R roots per step (their lookups issue together).  The locations and
+ * magnitudes go out as a 32-byte record per codeword for rs_apply_k.
+ */
+__global__ __launch_bounds__(FWG, FORNEY_WAVES) void rs_forney_k(const RsDevTables *__restrict__ T, RsCorrParams P,
+                                                       uint8_t *data, size_t dstride, uint8_t *parity, size_t pstride,
+                                                       size_t count, const uint8_t *__restrict__ lam,
+                                                       const uint8_t *__restrict__ om,
+                                                       uint8_t *__restrict__ roots,
+                                                       const uint8_t *__restrict__ meta, uint8_t *__restrict__ ok,
+                                                       uint8_t *__restrict__ corrected)
+{
+    __shared__ uint32_t lgf[512 * 32];
+    fill_gfa(lgf, T);
+    __syncthreads();
+    const GfA gf{lds_addr(lgf) + 4u * (threadIdx.x & 31u) + 1u};
+    const int32_t pad = P.pad;
+
+    for (size_t base = (size_t)blockIdx.x * FWG; base < count; base += (size_t)gridDim.x * FWG) {
+        const size_t cw = base + threadIdx.x;
+        const bool valid = cw < count;
+        const uint32_t st = valid ? meta[cw] : 0u;
+        const bool fast = (st >> 5) == RS_ST_FAST;
+        if (__ballot(fast) == 0ull)
+            continue;
+        const uint32_t deg = fast ? (st & 31u) : 0u;
+        uint4 o4 = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu), l4 = o4;
+        uint32_t rb[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        if (fast) {
+            o4 = reinterpret_cast<const uint4 *>(om)[cw];
+            l4 = reinterpret_cast<const uint4 *>(lam)[cw];
+            const uint4 *r4 = reinterpret_cast<const uint4 *>(roots + cw * 32u);
+            const uint4 ra = r4[0], rc = r4[1];
+            rb[0] = ra.x, rb[1] = ra.y, rb[2] = ra.z, rb[3] = ra.w;
+            rb[4] = rc.x, rb[5] = rc.y, rb[6] = rc.z, rb[7] = rc.w;
+        }
+        const uint32_t ow[4] = {o4.x, o4.y, o4.z, o4.w}, lw[4] = {l4.x, l4.y, l4.z, l4.w};
+        /* address-form logs: Omega_m packed two per register, and the
+         * derivative terms Lambda_(2h+1) for 2h <= dtop = (deg - 1) & ~1 */
+        uint32_t omp[8], lod[4];
+#pragma unroll
+        for (int m = 0; m < 16; m += 2)
+            omp[m >> 1] = gf.afrom((ow[m >> 2] >> (8 * (m & 3))) & 0xffu) |
+                          (gf.afrom((ow[(m + 1) >> 2] >> (8 * ((m + 1) & 3))) & 0xffu) << 16);
+        const uint32_t dtop = deg ? (deg - 1u) & ~1u : 0u;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int jl = 4 * q + 1, jh = 4 * q + 3; /* Lambda_j = byte j - 1 */
+            const uint32_t lo =
+                (uint32_t)(4 * q) <= dtop ? gf.afrom((lw[(jl - 1) >> 2] >> (8 * ((jl - 1) & 3))) & 0xffu) : gf.az();
+            const uint32_t hi =
+                (uint32_t)(4 * q + 2) <= dtop ? gf.afrom((lw[(jh - 1) >> 2] >> (8 * ((jh - 1) & 3))) & 0xffu)
+                                              : gf.az();
+            lod[q] = lo | (hi << 16);
+        }
+#define OMLOG(m) (((m) & 1) ? (omp[(m) >> 1] >> 16) : (omp[(m) >> 1] & 0xffffu))
+#define LODD(h) (((h) & 1) ? (lod[(h) >> 1] >> 16) : (lod[(h) >> 1] & 0xffffu))
+        const uint32_t degmax = wave_max(deg);
+        const uint32_t nir = max(degmax, wave_max(dtop) + 1u); /* powers i m needed: m < nir */
+        RootIter it;
+        it.init(rb);
+        /* phase 1: every root's location byte and magnitude, packed four per
+         * register (the roots' loop is unrolled: FORNEY_R per step, steps past
+         * the wave's degree skipped) */
+        uint32_t posp[4] = {0, 0, 0, 0}, magp[4] = {0, 0, 0, 0};
+        uint32_t fixed = 0;
+#pragma unroll
+        for (int n = 0; n < 16; n += FORNEY_R) {
+            if ((uint32_t)n >= degmax) /* uniform */
+                continue;
+            uint32_t ir[FORNEY_R];
+#pragma unroll
+            for (int t = 0; t < FORNEY_R; ++t)
+                ir[t] = it.next(); /* 255 past the last root */
+            /* powers alpha^(i m) as plain scaled logs 128 (i m mod 255), even
+             * and odd m in two chains */
+            uint32_t i2[FORNEY_R], ie[FORNEY_R], io[FORNEY_R], nm[FORNEY_R], den[FORNEY_R];
+#pragma unroll
+            for (int t = 0; t < FORNEY_R; ++t) {
+                const uint32_t i1 = ir[t] == 255u ? 0u : ir[t];
+                i2[t] = red(i1 + i1) << 7;
+                ie[t] = 0;
+                io[t] = i1 << 7;
+                nm[t] = 0;
+                den[t] = 0;
+            }
+#pragma unroll
+            for (int m0 = 0; m0 < 16; m0 += 4) {
+                if ((uint32_t)m0 < nir) {
+#pragma unroll
+                    for (int m = m0; m < m0 + 4; m += 2) {
+#pragma unroll
+                        for (int t = 0; t < FORNEY_R; ++t) {
+                            nm[t] ^= gf.expa(OMLOG(m) + ie[t]);
+                            den[t] ^= gf.expa(LODD(m >> 1) + ie[t]);
+                            nm[t] ^= gf.expa(OMLOG(m + 1) + io[t]);
+                            const uint32_t te = ie[t] + i2[t], to = io[t] + i2[t];
+                            ie[t] = min(te, te - 255u * 128u);
+                            io[t] = min(to, to - 255u * 128u);
+                        }
+                    }
+                }
+                __builtin_amdgcn_sched_barrier(0); /* one group of powers at a time: registers */
+            }
+#pragma unroll
+            for (int t = 0; t < FORNEY_R; ++t) {
+                const uint32_t ln2 = mod255((uint32_t)((int32_t)ir[t] * ((int32_t)P.fcr - 1) + (int32_t)RS_NN));
+                const uint32_t lden = gf.plog(gf.loga(den[t])); /* log 0 = 255 in the reference: no den = 0 guard */
+                const uint32_t lm = (gf.plog(gf.loga(nm[t])) + ln2 + RS_NN - lden) % 255u;
+                const bool z = (uint32_t)(n + t) < deg && nm[t] != 0u; /* zero numerator: no correction, not counted */
+                fixed += z ? 1u : 0u;
+                const uint32_t p = (uint32_t)((int32_t)((ir[t] * P.iprim + 254u) % 255u) - pad); /* < size + 32 */
+                posp[(n + t) >> 2] |= p << (8 * ((n + t) & 3));
+                magp[(n + t) >> 2] |= (z ? gf.exp(lm) : 0u) << (8 * ((n + t) & 3));
+            }
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        /* the corrections go to rs_apply_k as a record: 16 location bytes,
+         * 16 magnitudes (0: nothing to apply); over the root map just read */
+        if (fast) {
+            uint4 *rec = reinterpret_cast<uint4 *>(roots + cw * 32u);
+            rec[0] = make_uint4(posp[0], posp[1], posp[2], posp[3]);
+            rec[1] = make_uint4(magp[0], magp[1], magp[2], magp[3]);
+        }
+#undef OMLOG
+#undef LODD
+        if (fast) {
+            ok[cw] = 1;
+            if (corrected)
+                corrected[cw] = (uint8_t)fixed;
+        }
+    }
+}
+
+/* ------------------------------------------------------------------------ */
+/* rs_apply_k: the corrections, src/decode.c:215-226                         */
+/* ------------------------------------------------------------------------ */
+
+/*
+ * One wave per 64 codewords.  Wire layout (255-byte rows back to back, data
+ * 16-byte aligned), whole waves: the wave's 16,320-byte block is read into
+ * LDS with coalesced 16-byte loads, each lane XORs its codeword's magnitudes
+ * in (ds_xor_b32), and the block is written back the same way -- 2 x 16 memory
+ * requests per wave-instruction row instead of one request per corrected
+ * byte (scattered byte read-modify-writes measured 0.15 ms per 2^20
+ * codewords with 16 errors, bound by the L2's request rate).  Other layouts
+ * and a batch's last partial wave correct byte by byte.  Locations are
+ * distinct (distinct roots), so the order of the corrections is immaterial.
+ */
+#define AWG 256                 /* 4 waves, 16,320 B of LDS each */
+#define ABLK (64u * 255u / 16u) /* 16-byte chunks per wave block: 1020 */
+
+__global__ __launch_bounds__(AWG) void rs_apply_k(const uint8_t *__restrict__ meta, const uint8_t *__restrict__ rec,
+                                                  uint8_t *data, size_t dstride, uint8_t *parity, size_t pstride,
+                                                  uint32_t size, size_t count, uint32_t wire)
+{
+    __shared__ uint4 img[AWG / 64][ABLK];
+    const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63u;
+    const size_t base = ((size_t)blockIdx.x * (AWG / 64) + w) * 64u;
+    if (base >= count)
+        return;
+    const size_t cw = base + lane;
+    const bool valid = cw < count;
+    const bool fast = valid && (meta[cw] >> 5) == RS_ST_FAST;
+    uint4 pos4 = make_uint4(0, 0, 0, 0), mag4 = pos4;
+    if (fast) {
+        const uint4 *r = reinterpret_cast<const uint4 *>(rec + cw * 32u);
+        pos4 = r[0];
+        mag4 = r[1];
+    }
+    if (__ballot(fast) == 0ull)
+        return;
+    const uint32_t pw[4] = {pos4.x, pos4.y, pos4.z, pos4.w}, mw[4] = {mag4.x, mag4.y, mag4.z, mag4.w};
+    if (wire && base + 64u <= count) { /* uniform */
+        const uint4 *src = reinterpret_cast<const uint4 *>(data + base * 255u);
+        uint4 *dst = reinterpret_cast<uint4 *>(data + base * 255u);
+        uint4 *im = img[w];
+#pragma unroll
+        for (uint32_t k = 0; k < 16; ++k) {
+            const uint32_t c = lane + 64u * k;
+            if (c < ABLK)
+                im[c] = src[c];
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        uint32_t *imw = reinterpret_cast<uint32_t *>(im);
+#pragma unroll
+        for (int n = 0; n < 16; ++n) {
+            const uint32_t mg = (mw[n >> 2] >> (8 * (n & 3))) & 0xffu;
+            if (mg) {
+                const uint32_t b = lane * 255u + ((pw[n >> 2] >> (8 * (n & 3))) & 0xffu);
+                atomicXor(imw + (b >> 2), mg << (8u * (b & 3u)));
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+        for (uint32_t k = 0; k < 16; ++k) {
+            const uint32_t c = lane + 64u * k;
+            if (c < ABLK)
+                dst[c] = im[c];
+        }
+    } else if (fast) {
+        uint8_t *cdata = data + cw * dstride, *cpar = parity + cw * pstride;
+#pragma unroll
+        for (int n = 0; n < 16; ++n) {
+            const uint32_t mg = (mw[n >> 2] >> (8 * (n & 3))) & 0xffu;
+            if (mg) {
+                const uint32_t p = (pw[n >> 2] >> (8 * (n & 3))) & 0xffu;
+                uint8_t *d = p < size ? cdata + p : cpar + (p - size);
+                *d = (uint8_t)(*d ^ mg);
+            }
+        }
+    }
+}
+
+/* ------------------------------------------------------------------------ */
+/* launchers                                                                 */
+/* ------------------------------------------------------------------------ */
+
+extern "C" hipError_t rsk_bm(const RsDevTables *tab, const RsSplitWs *ws, size_t count, uint8_t *ok,
+                             uint8_t *corrected, int num_cu, hipStream_t stream)
+{
+    if (count == 0)
+        return hipSuccess;
+    hipLaunchKernelGGL(rs_bm_k, dim3(fast_grid(count, num_cu)), dim3(FWG), 0, stream, tab, ws->syn, count, ws->lam,
+                       ws->om, ws->meta, ws->list, ws->nlist, ok, corrected);
+    return hipGetLastError();
+}
+
+extern "C" hipError_t rsk_chien(const RsDevTables *tab, const RsCorrParams *prm, const RsSplitWs *ws, size_t count,
+                                uint8_t *ok, uint8_t *corrected, int num_cu, hipStream_t stream)
+{
+    if (count == 0)
+        return hipSuccess;
+    hipLaunchKernelGGL(rs_chien_k, dim3(fast_grid(count, num_cu)), dim3(FWG), 0, stream, tab, *prm, count, ws->lam,
+                       ws->meta, ws->roots, ok, corrected);
+    return hipGetLastError();
+}
+
+extern "C" hipError_t rsk_forney(const RsDevTables *tab, const RsCorrParams *prm, const RsSplitWs *ws, uint8_t *data,
+                                 size_t dstride, uint8_t *parity, size_t pstride, size_t count, uint8_t *ok,
+                                 uint8_t *corrected, int num_cu, hipStream_t stream)
+{
+    if (count == 0)
+        return hipSuccess;
+    hipLaunchKernelGGL(rs_forney_k, dim3(fast_grid(count, num_cu)), dim3(FWG), 0, stream, tab, *prm, data, dstride,
+                       parity, pstride, count, ws->lam, ws->om, ws->roots, ws->meta, ok, corrected);
+    return hipGetLastError();
+}
+
+extern "C" hipError_t rsk_apply(const RsCorrParams *prm, const RsSplitWs *ws, uint8_t *data, size_t dstride,
+                                uint8_t *parity, size_t pstride, size_t count, hipStream_t stream)
+{
+    if (count == 0)
+        return hipSuccess;
+    const uint32_t wire = prm->size == 223u && dstride == 255u && pstride == 255u && parity == data + 223 &&
+                          (reinterpret_cast<uintptr_t>(data) & 15u) == 0u;
+    const size_t waves = (count + 63) / 64;
+    hipLaunchKernelGGL(rs_apply_k, dim3((uint32_t)((waves + AWG / 64 - 1) / (AWG / 64))), dim3(AWG), 0, stream,
+                       ws->meta, ws->roots, data, dstride, parity, pstride, prm->size, count, wire);
+    return hipGetLastError();
+}

@@ -398,8 +398,11 @@ template <int MODE, int PATH>
 __global__ __launch_bounds__(LFSR_WG) void rs_lfsr_k(const RsDevTables *__restrict__ T,
                                                       const uint8_t *__restrict__ data, size_t dstride,
                                                       uint8_t *__restrict__ parity, size_t pstride, uint32_t size,
-                                                      size_t count, uint8_t *__restrict__ out)
+                                                      size_t count, uint8_t *__restrict__ out,
+                                                      uint32_t *__restrict__ reset)
 {
+    if (reset && blockIdx.x == 0 && threadIdx.x == 0)
+        *reset = 0u; /* the split decode's list length, before any later launch on the stream */
     __shared__ uint4 lds[512 * LFSR_REPL + (MODE == MODE_SYNDROME ? 32 * 2 * 2 * 16 : 0)];
     for (uint32_t t = threadIdx.x; t < 512u * LFSR_REPL; t += LFSR_WG)
         lds[t] = T->lfsr[t / LFSR_REPL];
@@ -490,7 +493,7 @@ static int persistent_grid(size_t count, int wg, int num_cu)
 template <int MODE>
 static hipError_t launch_lfsr(const RsDevTables *tab, const uint8_t *data, size_t dstride, const uint8_t *parity,
                               size_t pstride, uint32_t size, size_t count, uint8_t *out, int num_cu,
-                              hipStream_t stream)
+                              hipStream_t stream, uint32_t *reset = nullptr)
 {
     if (count == 0)
         return hipSuccess;
@@ -498,13 +501,13 @@ static hipError_t launch_lfsr(const RsDevTables *tab, const uint8_t *data, size_
     uint8_t *par = const_cast<uint8_t *>(parity);
     if (size != FULL_K)
         hipLaunchKernelGGL((rs_lfsr_k<MODE, PATH_GENERIC>), grid, block, 0, stream, tab, data, dstride, par, pstride,
-                           size, count, out);
+                           size, count, out, reset);
     else if (MODE != MODE_ENCODE && parity == data + FULL_K && pstride == dstride)
         hipLaunchKernelGGL((rs_lfsr_k<MODE, PATH_CONTIG>), grid, block, 0, stream, tab, data, dstride, par, pstride,
-                           size, count, out);
+                           size, count, out, reset);
     else
         hipLaunchKernelGGL((rs_lfsr_k<MODE, PATH_SPLIT>), grid, block, 0, stream, tab, data, dstride, par, pstride,
-                           size, count, out);
+                           size, count, out, reset);
     return hipGetLastError();
 }
 
@@ -519,6 +522,13 @@ extern "C" hipError_t rsk_syndrome(const RsDevTables *tab, const uint8_t *data, 
                                    hipStream_t stream)
 {
     return launch_lfsr<MODE_SYNDROME>(tab, data, dstride, parity, pstride, size, count, syn, num_cu, stream);
+}
+
+extern "C" hipError_t rsk_syndrome_reset(const RsDevTables *tab, const uint8_t *data, size_t dstride,
+                                         const uint8_t *parity, size_t pstride, uint32_t size, size_t count,
+                                         uint8_t *syn, uint32_t *reset, int num_cu, hipStream_t stream)
+{
+    return launch_lfsr<MODE_SYNDROME>(tab, data, dstride, parity, pstride, size, count, syn, num_cu, stream, reset);
 }
 
 /* poly-form syndromes (rsk_syndrome's output) -> the reference's log form:

@@ -1,0 +1,179 @@
+"""GPU parity of the split error-mode decode (rs_fast.hip: rs_bm_k, rs_chien_k,
+rs_forney_k, and the general kernel over the codewords they hand on).
+
+POPORON_AMD_DECODE_PATH (read at poporon_create) forces the split kernels or
+the single correction kernel whatever the batch size, so both paths meet the
+same inputs; the expected values come from the golden fixtures (the compiled
+reference, tools/gen_golden.py) or the pinned CPU oracle.  Everything is
+compared bit-exactly: bytes, the bool result and corrected_num.
+"""
+import numpy as np
+import pytest
+
+import libpoporon_amd as P
+
+pytestmark = pytest.mark.gpu
+
+NR = 32
+PATHS = ["split", "single"]
+
+
+def _handle(monkeypatch, path, params=(8, 0x11D, 1, 1, 32)):
+    if P.device_count() == 0:
+        pytest.fail("no HIP device: GPU tests must run on the MI355X box")
+    monkeypatch.setenv("POPORON_AMD_DECODE_PATH", path)
+    h = P.Poporon(*params)
+    assert h.supported
+    return h
+
+
+def _same(got, want):
+    ok, cor, d, p = got
+    ook, ocor, od, op = want
+    assert (ok == ook).all(), np.nonzero(ok != ook)[0][:8]
+    assert (cor == ocor).all(), np.nonzero(cor != ocor)[0][:8]
+    assert (d == od).all() and (p == op).all()
+
+
+def test_split_golden(monkeypatch, golden):
+    h = _handle(monkeypatch, "split")
+    sizes = golden["dec_size"]
+    for s in np.unique(sizes):
+        sel = np.nonzero(sizes == s)[0]
+        s = int(s)
+        ok, cor, d, p = h.decode_batch(golden["dec_in"][sel, :s], golden["dec_in"][sel, s:s + NR])
+        assert (ok == golden["dec_ok"][sel]).all(), s
+        assert (cor == golden["dec_cor"][sel]).all(), s
+        assert (np.concatenate([d, p], 1) == golden["dec_out"][sel, :s + NR]).all(), s
+
+
+@pytest.mark.parametrize("path", PATHS)
+@pytest.mark.parametrize("size", [223, 200, 17, 1])
+def test_split_random_vs_oracle(monkeypatch, oracle_default, path, size):
+    """0..20 random errors (clean, correctable and beyond-capacity codewords
+    side by side in every wave), shortened codes included."""
+    h = _handle(monkeypatch, path)
+    rng = np.random.default_rng(1000 + size)
+    n = 12000
+    data = rng.integers(0, 256, (n, size), dtype=np.uint8)
+    cw = np.concatenate([data, h.encode_batch(data)], 1)
+    L = size + NR
+    ne = rng.integers(0, min(21, L + 1), n)
+    for c in range(n):
+        pos = rng.permutation(L)[: ne[c]]
+        cw[c, pos] ^= rng.integers(1, 256, ne[c], dtype=np.uint8)
+    got = h.decode_batch(cw[:, :size], cw[:, size:])
+    _same(got, oracle_default.decode_batch(cw[:, :size], cw[:, size:]))
+
+
+@pytest.mark.parametrize("path", PATHS)
+def test_split_beyond_capacity_vs_oracle(monkeypatch, oracle_default, path):
+    """14..32 errors: codewords the split kernels hand to the general kernel
+    (L > 16, deg != L, a locator past x^16) and the miscorrections the
+    reference makes, bit for bit."""
+    h = _handle(monkeypatch, path)
+    rng = np.random.default_rng(77)
+    n = 30000
+    data = rng.integers(0, 256, (n, 223), dtype=np.uint8)
+    cw = np.concatenate([data, h.encode_batch(data)], 1)
+    for c in range(n):
+        ne = int(rng.integers(14, 33))
+        pos = rng.permutation(255)[:ne]
+        cw[c, pos] ^= rng.integers(1, 256, ne, dtype=np.uint8)
+    got = h.decode_batch(cw[:, :223], cw[:, 223:])
+    want = oracle_default.decode_batch(cw[:, :223], cw[:, 223:])
+    assert want[0].sum() > n // 10 and (~want[0].astype(bool)).sum() > n // 10
+    _same(got, want)
+
+
+def test_split_constructed_miscorrections(monkeypatch, golden, oracle_default):
+    """The golden file's constructed miscorrections (words next to another
+    codeword) and beyond-capacity failures, repeated to fill whole waves."""
+    h = _handle(monkeypatch, "split")
+    sel = np.nonzero(golden["dec_size"] == 223)[0]
+    inp = np.tile(golden["dec_in"][sel], (8, 1))
+    got = h.decode_batch(inp[:, :223], inp[:, 223:NR + 223])
+    _same(got, oracle_default.decode_batch(inp[:, :223], inp[:, 223:NR + 223]))
+
+
+@pytest.mark.parametrize("params", [(8, 0x11D, 0, 1, 32), (8, 0x11D, 2, 1, 32), (8, 0x11D, 1, 2, 32),
+                                    (8, 0x187, 1, 1, 32), (8, 0x11D, 5, 7, 32)])
+def test_split_other_parameters_vs_oracle(monkeypatch, params):
+    from oracle import Oracle
+    o = Oracle(*params)
+    h = _handle(monkeypatch, "split", params)
+    rng = np.random.default_rng(sum(params))
+    n = 9000
+    data = rng.integers(0, 256, (n, 223), dtype=np.uint8)
+    par = h.encode_batch(data)
+    assert (par == o.encode_batch(data)).all()
+    cw = np.concatenate([data, par], 1)
+    for c in range(n):
+        ne = int(rng.integers(0, 23))
+        pos = rng.permutation(255)[:ne]
+        cw[c, pos] ^= rng.integers(1, 256, ne, dtype=np.uint8)
+    _same(h.decode_batch(cw[:, :223], cw[:, 223:]), o.decode_batch(cw[:, :223], cw[:, 223:]))
+
+
+@pytest.mark.parametrize("offset,stride", [(1, 257), (3, 256), (0, 255)])
+def test_split_device_strides(monkeypatch, oracle_default, offset, stride):
+    import torch
+    h = _handle(monkeypatch, "split")
+    rng = np.random.default_rng(stride + offset)
+    n = 20000
+    data = rng.integers(0, 256, (n, 223), dtype=np.uint8)
+    cw = np.concatenate([data, oracle_default.encode_batch(data)], 1)
+    for c in range(n):
+        ne = int(rng.integers(0, 19))
+        pos = rng.permutation(255)[:ne]
+        cw[c, pos] ^= rng.integers(1, 256, ne, dtype=np.uint8)
+    buf = np.zeros(offset + n * stride, np.uint8)
+    rows = buf[offset:].reshape(n, stride)
+    rows[:, :255] = cw
+    d = torch.from_numpy(buf).cuda()
+    ok = torch.zeros(n, dtype=torch.uint8, device="cuda")
+    cor = torch.zeros(n, dtype=torch.uint8, device="cuda")
+    base = d.data_ptr() + offset
+    s = torch.cuda.current_stream().cuda_stream
+    h.decode_batch_device(base, stride, base + 223, stride, 223, n, ok.data_ptr(), cor.data_ptr(), stream=s)
+    torch.cuda.synchronize()
+    out = d.cpu().numpy()[offset:].reshape(n, stride)
+    want = oracle_default.decode_batch(cw[:, :223], cw[:, 223:])
+    _same((ok.cpu().numpy(), cor.cpu().numpy(), out[:, :223], out[:, 223:255]), want)
+    assert (out[:, 255:] == 0).all()  # bytes between rows untouched
+
+
+def test_split_kernels_timed(monkeypatch, torch_cuda_split):
+    """A 2^16 batch with 16 errors each runs the split kernels (timing ids
+    1, 4..8) and not the single kernel; the list kernel finds nothing to do."""
+    torch = torch_cuda_split
+    h = _handle(monkeypatch, "split")
+    n = 1 << 16
+    g = torch.Generator(device="cuda")
+    g.manual_seed(5)
+    cw = torch.randint(0, 256, (n, 255), dtype=torch.uint8, device="cuda", generator=g)
+    s = torch.cuda.current_stream().cuda_stream
+    base = cw.data_ptr()
+    h.encode_batch_device(base, 255, base + 223, 255, 223, n, s)
+    clean = cw.clone()
+    pos = torch.rand((n, 255), device="cuda", generator=g).topk(16, dim=1).indices
+    mag = torch.randint(1, 256, (n, 16), dtype=torch.uint8, device="cuda", generator=g)
+    cw.scatter_(1, pos, cw.gather(1, pos) ^ mag)
+    ok = torch.zeros(n, dtype=torch.uint8, device="cuda")
+    cor = torch.zeros(n, dtype=torch.uint8, device="cuda")
+    h.timing(True)
+    h.decode_batch_device(base, 255, base + 223, 255, 223, n, ok.data_ptr(), cor.data_ptr(), stream=s)
+    torch.cuda.synchronize()
+    t = {k: h.timing_read(k) for k in P.KERNEL_NAMES}
+    h.timing(False)
+    assert torch.equal(cw, clean) and int(ok.sum()) == n and bool((cor == 16).all())
+    for k in (P.KERNEL_REMAINDER, P.KERNEL_BM, P.KERNEL_CHIEN, P.KERNEL_FORNEY, P.KERNEL_APPLY, P.KERNEL_LIST):
+        assert t[k][1] == 1, (k, t[k])
+    assert t[P.KERNEL_CORRECT][1] == 0
+
+
+@pytest.fixture(scope="module")
+def torch_cuda_split():
+    import torch
+    assert torch.cuda.is_available()
+    return torch

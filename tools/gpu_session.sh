@@ -33,7 +33,7 @@ for step in "$@"; do
         i=0
         for grp in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE" \
                    "SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAIT_ANY" \
-                   "SQ_INSTS_SMEM SQ_INSTS_BRANCH SQ_IFETCH SQ_ACTIVE_INST_LDS SQ_INST_CYCLES_SALU" \
+                   "SQ_INSTS_SMEM SQ_INSTS_BRANCH SQ_IFETCH SQ_ACTIVE_INST_LDS SQ_INST_CYCLES_SALU SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS" \
                    "FETCH_SIZE" "WRITE_SIZE"; do
             run pmc$i 300 rocprofv3 --pmc $grp -d gpurun_out/pmc$i -o pmc --output-format csv -- \
                 python3 tools/kernel_driver.py --reps 3

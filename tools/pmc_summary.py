@@ -29,11 +29,16 @@ NAMES = {"rs_lfsr_k<0>": "rs_lfsr_k<false> (encode)", "rs_lfsr_k<1>": "rs_lfsr_k
          "rs_lfsr_k<1, 2>": "rs_lfsr_k<true> (remainder)", "rs_lfsr_k<1, 1>": "rs_lfsr_k<true> (remainder)",
          "rs_correct_k<unsigned char, false>": "rs_correct_k (BM/Chien/Forney)",
          "rs_correct_k<unsigned char, true>": "rs_correct_k (erasure, u8 slots)",
-         "rs_correct_k<unsigned int, true>": "rs_correct_k (erasure, u32 slots)"}
+         "rs_correct_k<unsigned int, true>": "rs_correct_k (erasure, u32 slots)",
+         "rs_bm_k": "rs_bm_k (BM/Omega)", "rs_chien_k": "rs_chien_k (Chien)",
+         "rs_forney_k": "rs_forney_k (Forney)", "rs_apply_k": "rs_apply_k (apply)"}
 
 
 def short(name):
     m = re.search(r"(rs_[a-z_]+<[^>]*>)", name)
+    if m:
+        return m.group(1)
+    m = re.search(r"\b(rs_(?:bm|chien|forney|apply)_k)\b", name)
     return m.group(1) if m else None
 
 
