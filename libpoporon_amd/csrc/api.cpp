@@ -482,6 +482,13 @@ static void build_tables(poporon_t *h)
             memcpy(&t.chien[(j - 1) * 256 + e], rowb, 16);
         }
     }
+    /* the split kernels' GF table image (rs_device.h) */
+    uint32_t *gfa = reinterpret_cast<uint32_t *>(t.gfa);
+    for (uint32_t x = 0; x < 512; x++)
+        for (uint32_t r = 0; r < 32; r++) {
+            const uint32_t la = x < 256u ? (x ? (uint32_t)t.log[x] * 128u + 4u * r + 1u : 128u * RS_Z0 + 4u * r) : 0u;
+            gfa[x * 32 + r] = ((uint32_t)t.exp2[x] << 8) | (la << 16);
+        }
     const char *fv = getenv("POPORON_AMD_FORCE_VERIFY");
     p.force_verify = (fv && fv[0] == '1') ? 1u : 0u;
     const char *sa = getenv("POPORON_AMD_STOP_AT"); /* profiling ablation only */

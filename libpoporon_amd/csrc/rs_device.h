@@ -44,7 +44,14 @@ struct RsDevTables {
      * locator term at 16 consecutive points for a coefficient of log e;
      * entry e = 255 (log of zero) is an all-zero row. */
     uint4 chien[16 * 256];
+    /* gfa: the LDS image of the split kernels' GF table (rs_fast.hip header),
+     * dword x * 32 + r for x < 512 and replica r < 32:
+     *   (exp2[x] << 8) | (la << 16),  la = 128 log x + 4r + 1 for 0 < x < 256,
+     *   128 RS_Z0 + 4r for x = 0, 0 for x >= 256
+     * (copied into LDS at address 0 by every workgroup: 4 uint4 per thread) */
+    uint4 gfa[512 * 32 / 4];
 };
+#define RS_Z0 200u /* zero sentinel row of gfa (rs_fast.hip) */
 
 /*
  * Parameters of the correction kernel (by value).  tr_start/tr_inc turn the
