@@ -49,9 +49,6 @@ typedef __attribute__((address_space(1))) const uint32_t gu32;
 #define LFSR_STAGGER 0 /* (experiment) odd waves sleep LFSR_STAGGER x 8128 cycles first */
 #endif
 #define LFSR_REPL 16
-#ifndef LFSR_UNALIGNED
-#define LFSR_UNALIGNED 0 /* 1: 16-byte loads at the rows' own alignment (UStream): measured slower */
-#endif
 
 /* ------------------------------------------------------------------------ */
 /* LFSR (encode / syndromes / check)                                        */
@@ -276,46 +273,6 @@ __device__ __forceinline__ uint32_t stream_byte(const Stream<N> &s, int i)
     return s.word(i >> 2) >> (8 * (i & 3));
 }
 
-/* Fixed-length stream of N message bytes in registers, loaded with 16-byte
- * accesses at the stream's own byte alignment (unaligned global dwordx4,
- * tools/probes/unaligned.hip): chunk c = bytes [16c, 16c + 16), except a
- * partial last chunk, loaded as the 16 bytes ending at byte N - 1 (no read
- * past the stream).  No realignment in registers: byte i is a compile-time
- * register and shift (the aligned-chunk Stream spends a two-level select and
- * an alignbyte, three half-rate VALU, per dword). */
-typedef unsigned u32x4u __attribute__((ext_vector_type(4), aligned(1)));
-typedef __attribute__((address_space(1))) const u32x4u gu32x4u;
-template <int N>
-struct UStream {
-    static constexpr int NCH = (N + 15) / 16;
-    static constexpr int TAIL = N % 16 ? N - 16 : -1; /* start byte of the overlapped last chunk */
-    uint32_t D[NCH * 4];
-    __device__ __forceinline__ void chunk(int, const NextSrc &) {} /* no refills (lfsr_stream's REFILL = false) */
-    __device__ __forceinline__ void load(const uint8_t *p)
-    {
-#pragma unroll
-        for (int c = 0; c < NCH; ++c) {
-            const int off = (c == NCH - 1 && TAIL >= 0) ? TAIL : 16 * c;
-            const u32x4u v = *(gu32x4u *)(uintptr_t)(p + off);
-            D[4 * c] = v.x;
-            D[4 * c + 1] = v.y;
-            D[4 * c + 2] = v.z;
-            D[4 * c + 3] = v.w;
-        }
-    }
-};
-
-template <int N>
-__device__ __forceinline__ uint32_t stream_byte(const UStream<N> &s, int i)
-{
-    constexpr int T = UStream<N>::TAIL;
-    if (T >= 0 && i >= 16 * (UStream<N>::NCH - 1)) {
-        const int j = i - T;
-        return s.D[4 * (UStream<N>::NCH - 1) + (j >> 2)] >> (8 * (j & 3));
-    }
-    return s.D[i >> 2] >> (8 * (i & 3));
-}
-
 /* The bytes [I0, I1) of s, starting at rotation R0 + I0; s is refilled with
  * the stream `next` in two batches of consecutive chunks (each batch's loads
  * of a row hit the same few cache lines back to back): chunks [0, NCH/2)
@@ -473,35 +430,6 @@ __global__ __launch_bounds__(LFSR_WG) void rs_lfsr_k(const RsDevTables *__restri
             il_bytes(P, X, 0);
             lfsr_epilogue<MODE>(P, synt, cw, parity, pstride, out);
         }
-    } else if (!PF && LFSR_UNALIGNED) {
-        /* 16-byte loads at the rows' own alignment (UStream) */
-        const NextSrc none(nullptr, false, nullptr);
-        for (size_t cw = cw0; cw < count; cw += step) {
-            uint32_t X[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-            uint32_t P[8];
-            if (PATH == PATH_CONTIG && MODE != MODE_ENCODE) {
-                UStream<FULL_K + RS_NR> sc;
-                sc.load(data + cw * dstride);
-                lfsr_stream<FULL_K + RS_NR, 0, 0, 128, false>(X, sc, none, tab);
-                lfsr_stream<FULL_K + RS_NR, 0, 128, FULL_K + RS_NR, false>(X, sc, none, tab);
-                il_bytes(P, X, (FULL_K + RS_NR) & 7);
-            } else {
-                UStream<FULL_K> sd;
-                sd.load(data + cw * dstride);
-                if (MODE != MODE_ENCODE) {
-                    lfsr_stream<FULL_K, 0, 0, 150, false>(X, sd, none, tab);
-                    UStream<RS_NR> sp;
-                    sp.load(parity + cw * pstride);
-                    lfsr_stream<FULL_K, 0, 150, FULL_K, false>(X, sd, none, tab);
-                    lfsr_stream<RS_NR, FULL_K, 0, RS_NR, false>(X, sp, none, tab);
-                    il_bytes(P, X, (FULL_K + RS_NR) & 7);
-                } else {
-                    lfsr_stream<FULL_K, 0, 0, FULL_K, false>(X, sd, none, tab);
-                    il_bytes(P, X, FULL_K & 7);
-                }
-            }
-            lfsr_epilogue<MODE>(P, synt, cw, parity, pstride, out);
-        }
     } else if (PATH == PATH_CONTIG && MODE != MODE_ENCODE) {
         /* data || parity as one 255-byte stream */
         Stream<FULL_K + RS_NR> sc;
@@ -556,282 +484,6 @@ __global__ __launch_bounds__(LFSR_WG) void rs_lfsr_k(const RsDevTables *__restri
     }
 }
 
-/* ------------------------------------------------------------------------ */
-/* Two codewords per lane (size 223)                                        */
-/* ------------------------------------------------------------------------ */
-
-/*
- * rs_lfsr2_k: the same LFSR, but every lane runs two codewords' shift
- * registers side by side (two independent dependency chains: the step's
- * table reads of one overlap the other's), and the message bytes stream in
- * 64-byte groups that are loaded one group ahead of use (the next codeword
- * pair's first group during the last group of this pair), so HBM traffic
- * overlaps the table work instead of coming in bulk rounds between codewords.
- * Loads and parity stores are 16-byte accesses at any byte alignment
- * (unaligned global dwordx4, probed: tools/probes/unaligned.hip), so a
- * group's dwords are message dwords as loaded.  Never reads past a row's
- * message: the 31-byte tail is loaded as bytes 192..207 and 207..222.
- */
-#ifndef LF2_TOUCH
-#define LF2_TOUCH 0
-#endif
-#ifndef LF2_TEST
-#define LF2_TEST 0
-#endif
-#ifndef LFSR_V2
-#define LFSR_V2 0
-#endif
-typedef unsigned u16b_t __attribute__((ext_vector_type(4), aligned(1)));
-typedef unsigned lds_u4 __attribute__((ext_vector_type(4)));
-typedef __attribute__((address_space(3))) const lds_u4 lds_u4p;
-/* ds_read_b128 from an LDS byte address */
-__device__ __forceinline__ lds_u4 lds_ld(uint32_t a) { return *(lds_u4p *)(size_t)a; }
-template <typename T> __device__ __forceinline__ uint32_t lds_addr_of(const T *p)
-{
-    return (uint32_t)(size_t)(__attribute__((address_space(3))) const T *)p;
-}
-typedef __attribute__((address_space(1))) const u16b_t gu16b;
-typedef __attribute__((address_space(1))) u16b_t gu16bw;
-
-/* LDS address of the two halves' replica row for feedback byte (x ^ d) & 0xff:
- * one full-rate v_bitop3 and one v_lshl_add (the compiler's own choice,
- * byte-select xor + shift + and_or, is three half-rate instructions) */
-__device__ __forceinline__ uint32_t il_addr(uint32_t x, uint32_t d, uint32_t base)
-{
-    const uint32_t fb = __builtin_amdgcn_bitop3_b32(x, d, 0xffu, 0x28); /* (x ^ d) & 0xff */
-    return (fb << 9) + base;                                           /* 2 x 16 replicas x 16 B per row */
-}
-
-/* two steps at rotation r for two independent registers: both chains' table
- * reads are issued before either is consumed */
-__device__ __forceinline__ void il_pair2(uint32_t (&XA)[8], uint32_t (&XB)[8], int r, uint32_t a0, uint32_t a1,
-                                         uint32_t b0, uint32_t b1, uint32_t base)
-{
-    const int i0 = r & 7, i1 = (r + 1) & 7;
-    uint32_t RaA[8], RaB[8], RbA[8], RbB[8];
-    {
-        const uint32_t pa = il_addr(XA[i0], a0, base), pb = il_addr(XB[i0], b0, base);
-        const lds_u4 ta = lds_ld(pa), ua = lds_ld(pa + 256u), tb = lds_ld(pb), ub = lds_ld(pb + 256u);
-        RaA[0] = ta.x, RaA[1] = ta.y, RaA[2] = ta.z, RaA[3] = ta.w, RaA[4] = ua.x, RaA[5] = ua.y, RaA[6] = ua.z,
-        RaA[7] = ua.w;
-        RaB[0] = tb.x, RaB[1] = tb.y, RaB[2] = tb.z, RaB[3] = tb.w, RaB[4] = ub.x, RaB[5] = ub.y, RaB[6] = ub.z,
-        RaB[7] = ub.w;
-    }
-    XA[i1] ^= RaA[0];
-    XB[i1] ^= RaB[0];
-    const uint32_t wA = XA[i0] >> 8, wB = XB[i0] >> 8;
-    {
-        const uint32_t pa = il_addr(XA[i1], a1, base), pb = il_addr(XB[i1], b1, base);
-        const lds_u4 ta = lds_ld(pa), ua = lds_ld(pa + 256u), tb = lds_ld(pb), ub = lds_ld(pb + 256u);
-        RbA[0] = ta.x, RbA[1] = ta.y, RbA[2] = ta.z, RbA[3] = ta.w, RbA[4] = ua.x, RbA[5] = ua.y, RbA[6] = ua.z,
-        RbA[7] = ua.w;
-        RbB[0] = tb.x, RbB[1] = tb.y, RbB[2] = tb.z, RbB[3] = tb.w, RbB[4] = ub.x, RbB[5] = ub.y, RbB[6] = ub.z,
-        RbB[7] = ub.w;
-    }
-#pragma unroll
-    for (int j = 1; j < 7; ++j) {
-        XA[(r + 1 + j) & 7] = xor3(XA[(r + 1 + j) & 7], RaA[j], RbA[j - 1]);
-        XB[(r + 1 + j) & 7] = xor3(XB[(r + 1 + j) & 7], RaB[j], RbB[j - 1]);
-    }
-    XA[i0] = xor3(wA, RaA[7], RbA[6]);
-    XB[i0] = xor3(wB, RaB[7], RbB[6]);
-    XA[i1] = (XA[i1] >> 8) ^ RbA[7];
-    XB[i1] = (XB[i1] >> 8) ^ RbB[7];
-}
-
-/* one step at rotation r for both registers */
-__device__ __forceinline__ void il_step2(uint32_t (&XA)[8], uint32_t (&XB)[8], int r, uint32_t a0, uint32_t b0,
-                                         uint32_t base)
-{
-    const int i0 = r & 7;
-    const uint32_t pa = il_addr(XA[i0], a0, base), pb = il_addr(XB[i0], b0, base);
-    const lds_u4 ta = lds_ld(pa), ua = lds_ld(pa + 256u), tb = lds_ld(pb), ub = lds_ld(pb + 256u);
-    const uint32_t RA[8] = {ta.x, ta.y, ta.z, ta.w, ua.x, ua.y, ua.z, ua.w};
-    const uint32_t RB[8] = {tb.x, tb.y, tb.z, tb.w, ub.x, ub.y, ub.z, ub.w};
-    XA[i0] = (XA[i0] >> 8) ^ RA[7];
-    XB[i0] = (XB[i0] >> 8) ^ RB[7];
-#pragma unroll
-    for (int k = 0; k < 7; ++k) {
-        XA[(r + 1 + k) & 7] ^= RA[k];
-        XB[(r + 1 + k) & 7] ^= RB[k];
-    }
-}
-
-/* 8 message dwords of bytes [32 g, 32 g + 32) (g < 6), or the 31-byte tail
- * (g = 6: dwords 0..3 = bytes 192..207, 4..7 = bytes 207..222) */
-#define LF2_NG 7
-template <int G>
-__device__ __forceinline__ void grp_load(uint32_t (&w)[8], const uint8_t *row)
-{
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {
-        const int off = G < 6 ? 32 * G + 16 * q : (q == 0 ? 192 : 207);
-#if LF2_TEST == 1 /* timing experiment only: 16-byte aligned loads (wrong bytes) */
-        const u16b_t v = *(gu16b *)((uintptr_t)(row + off) & ~(uintptr_t)15);
-#elif LF2_TEST == 2 /* timing experiment only: no loads */
-        const u16b_t v = {(uint32_t)(uintptr_t)row, (uint32_t)off, 3u, 4u};
-#else
-        const u16b_t v = *(gu16b *)(uintptr_t)(row + off);
-#endif
-        w[4 * q] = v.x;
-        w[4 * q + 1] = v.y;
-        w[4 * q + 2] = v.z;
-        w[4 * q + 3] = v.w;
-    }
-}
-
-/* message byte i of group G (any upper bits) */
-template <int G>
-__device__ __forceinline__ uint32_t grp_byte(const uint32_t (&w)[8], int i)
-{
-    if (G < 6 || i < 16)
-        return w[i >> 2] >> (8 * (i & 3));
-    const int j = i - 16 + 1; /* byte j of the second tail load */
-    return w[4 + (j >> 2)] >> (8 * (j & 3));
-}
-
-/* the group's steps for both codewords (rotation 32 G = 0 mod 8) */
-template <int G>
-__device__ __forceinline__ void grp_run(uint32_t (&XA)[8], uint32_t (&XB)[8], const uint32_t (&wa)[8],
-                                        const uint32_t (&wb)[8], uint32_t base)
-{
-    constexpr int NB = G < 6 ? 32 : 31;
-    static_for<0, NB - 1, 2>([&](auto ic) __attribute__((always_inline)) {
-        constexpr int i = decltype(ic)::value;
-        il_pair2(XA, XB, i, grp_byte<G>(wa, i), grp_byte<G>(wa, i + 1), grp_byte<G>(wb, i), grp_byte<G>(wb, i + 1),
-                 base);
-    });
-    if constexpr (NB & 1)
-        il_step2(XA, XB, NB - 1, grp_byte<G>(wa, NB - 1), grp_byte<G>(wb, NB - 1), base);
-}
-
-/* the 32 parity bytes (syndrome modes), rotation 223 on entry */
-__device__ __forceinline__ void par_run(uint32_t (&XA)[8], uint32_t (&XB)[8], const uint32_t (&pa)[8],
-                                        const uint32_t (&pb)[8], uint32_t base)
-{
-    static_for<0, RS_NR, 2>([&](auto ic) __attribute__((always_inline)) {
-        constexpr int i = decltype(ic)::value;
-        il_pair2(XA, XB, FULL_K + i, pa[i >> 2] >> (8 * (i & 3)), pa[(i + 1) >> 2] >> (8 * ((i + 1) & 3)),
-                 pb[i >> 2] >> (8 * (i & 3)), pb[(i + 1) >> 2] >> (8 * ((i + 1) & 3)), base);
-    });
-}
-
-__device__ __forceinline__ void par_load(uint32_t (&p)[8], const uint8_t *q)
-{
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-        const u16b_t v = *(gu16b *)(uintptr_t)(q + 16 * h);
-        p[4 * h] = v.x;
-        p[4 * h + 1] = v.y;
-        p[4 * h + 2] = v.z;
-        p[4 * h + 3] = v.w;
-    }
-}
-
-template <int MODE>
-__device__ __forceinline__ void lfsr2_out(const uint32_t (&P)[8], const uint4 *__restrict__ synt, size_t cw,
-                                          uint8_t *__restrict__ parity, size_t pstride, uint8_t *__restrict__ out)
-{
-    if (MODE == MODE_ENCODE) {
-        gu16bw *o = (gu16bw *)(uintptr_t)(parity + cw * pstride);
-        const u16b_t a = {P[0], P[1], P[2], P[3]}, b = {P[4], P[5], P[6], P[7]};
-        o[0] = a;
-        o[1] = b;
-    } else {
-        lfsr_epilogue<MODE>(P, synt, cw, parity, pstride, out);
-    }
-}
-
-template <int MODE>
-__global__ __launch_bounds__(LFSR_WG) void rs_lfsr2_k(const RsDevTables *__restrict__ T,
-                                                       const uint8_t *__restrict__ data, size_t dstride,
-                                                       uint8_t *__restrict__ parity, size_t pstride, size_t count,
-                                                       uint8_t *__restrict__ out, uint32_t *__restrict__ reset)
-{
-    if (reset && blockIdx.x == 0 && threadIdx.x == 0)
-        *reset = 0u; /* the split decode's list length, before any later launch on the stream */
-    __shared__ uint4 lds[512 * LFSR_REPL + (MODE != MODE_ENCODE ? 32 * 2 * 2 * 16 : 0)];
-    for (uint32_t t = threadIdx.x; t < 512u * LFSR_REPL; t += LFSR_WG)
-        lds[t] = T->lfsr[t / LFSR_REPL];
-    if (MODE != MODE_ENCODE)
-        for (uint32_t t = threadIdx.x; t < 32u * 2 * 2 * 16; t += LFSR_WG)
-            lds[512 * LFSR_REPL + t] = T->synt[t];
-    __syncthreads();
-    const uint4 *synt = lds + 512 * LFSR_REPL;
-
-    /* pair k of this lane: codewords base_k + tid and base_k + tid + LFSR_WG */
-    const uint32_t base = lds_addr_of(lds) + 16u * (threadIdx.x & (LFSR_REPL - 1));
-    const size_t step = (size_t)gridDim.x * (2 * LFSR_WG);
-    size_t cw = (size_t)blockIdx.x * (2 * LFSR_WG) + threadIdx.x;
-    if (cw >= count)
-        return;
-    auto rowp = [&](size_t c) __attribute__((always_inline)) { return data + (c < count ? c : 0) * dstride; };
-    uint32_t ga[8], gb[8], na[8], nb[8];
-    grp_load<0>(ga, rowp(cw));
-    grp_load<0>(gb, rowp(cw + LFSR_WG));
-    for (; cw < count; cw += step) {
-        const size_t cb = cw + LFSR_WG;
-        const uint8_t *ra = rowp(cw), *rb = rowp(cb);
-        uint32_t XA[8] = {0, 0, 0, 0, 0, 0, 0, 0}, XB[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-        uint32_t pa[8], pb[8];
-#if LF2_TOUCH
-        /* the next pair's rows pulled into the caches in one burst per row
-         * (the group loads then hit L2 / MALL instead of scattering small
-         * reads over open DRAM pages); consumed at the end of the pair */
-        uint32_t touch = 0;
-        {
-            const uint8_t *ta = rowp(cw + step), *tb = rowp(cb + step);
-#pragma unroll
-            for (int q = 0; q < 4; ++q)
-                touch ^= *(const __attribute__((address_space(1))) uint32_t *)(uintptr_t)(ta + 64 * q) ^
-                         *(const __attribute__((address_space(1))) uint32_t *)(uintptr_t)(tb + 64 * q);
-        }
-#endif
-        /* group g runs while group g + 1 (the next pair's group 0 after the
-         * last) is in flight; the buffers alternate at compile time */
-        static_for<0, LF2_NG, 1>([&](auto gc) __attribute__((always_inline)) {
-            constexpr int G = decltype(gc)::value;
-            uint32_t(&cur_a)[8] = (G & 1) ? na : ga;
-            uint32_t(&cur_b)[8] = (G & 1) ? nb : gb;
-            uint32_t(&nxt_a)[8] = (G & 1) ? ga : na;
-            uint32_t(&nxt_b)[8] = (G & 1) ? gb : nb;
-            if constexpr (G + 1 < LF2_NG) {
-                grp_load<G + 1>(nxt_a, ra);
-                grp_load<G + 1>(nxt_b, rb);
-            } else {
-                grp_load<0>(nxt_a, rowp(cw + step));
-                grp_load<0>(nxt_b, rowp(cb + step));
-                if (MODE != MODE_ENCODE) {
-                    par_load(pa, parity + (cw < count ? cw : 0) * pstride);
-                    par_load(pb, parity + (cb < count ? cb : 0) * pstride);
-                }
-            }
-            grp_run<G>(XA, XB, cur_a, cur_b, base);
-        });
-        /* LF2_NG is odd: the next pair's group 0 is in na / nb */
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-            ga[k] = na[k];
-            gb[k] = nb[k];
-        }
-        uint32_t PA[8], PB[8];
-#if LF2_TOUCH
-        asm volatile("" ::"v"(touch));
-#endif
-        if (MODE != MODE_ENCODE) {
-            par_run(XA, XB, pa, pb, base);
-            il_bytes(PA, XA, (FULL_K + RS_NR) & 7);
-            il_bytes(PB, XB, (FULL_K + RS_NR) & 7);
-        } else {
-            il_bytes(PA, XA, FULL_K & 7);
-            il_bytes(PB, XB, FULL_K & 7);
-        }
-        lfsr2_out<MODE>(PA, synt, cw, parity, pstride, out);
-        if (cb < count)
-            lfsr2_out<MODE>(PB, synt, cb, parity, pstride, out);
-    }
-}
-
 static int persistent_grid(size_t count, int wg, int num_cu)
 {
     size_t need = (count + wg - 1) / wg;
@@ -851,9 +503,6 @@ static hipError_t launch_lfsr(const RsDevTables *tab, const uint8_t *data, size_
     if (size != FULL_K)
         hipLaunchKernelGGL((rs_lfsr_k<MODE, PATH_GENERIC>), grid, block, 0, stream, tab, data, dstride, par, pstride,
                            size, count, out, reset);
-    else if (LFSR_V2)
-        hipLaunchKernelGGL((rs_lfsr2_k<MODE>), dim3(persistent_grid(count, 2 * LFSR_WG, num_cu)), block, 0, stream,
-                           tab, data, dstride, par, pstride, count, out, reset);
     else if (MODE != MODE_ENCODE && parity == data + FULL_K && pstride == dstride)
         hipLaunchKernelGGL((rs_lfsr_k<MODE, PATH_CONTIG>), grid, block, 0, stream, tab, data, dstride, par, pstride,
                            size, count, out, reset);
