@@ -751,10 +751,18 @@ __global__ __launch_bounds__(FWG, 8) void rs_chien_k(const RsDevTables *__restri
             A[k] = cb + (e << 8) + (jm << 4);
             inc[k] = e == 255u ? WRAP : (jm == 15u ? 256u : (jm + 1u) << 12);
         }
-        /* the map's words go to memory as they come (registers are short);
-         * the pad check below reads them back */
-        uint32_t *rmap = reinterpret_cast<uint32_t *>(roots + (valid ? cw : 0) * 32u);
-        uint32_t cnt = 0;
+        /* the roots as a byte list (src/decode.c:117-141 order: i' = 1..254,
+         * then i = 255), pushed in at byte 0 as they are found (newest
+         * first); Forney reads them by compile-time index instead of walking
+         * a bitmap (the walk cost rs_forney_k 38 of its 97 us) */
+        uint32_t L[4] = {0, 0, 0, 0};
+        uint32_t cnt = 0, z0 = 0;
+        auto push = [&](uint32_t v) __attribute__((always_inline)) {
+            L[3] = __builtin_amdgcn_alignbyte(L[3], L[2], 3);
+            L[2] = __builtin_amdgcn_alignbyte(L[2], L[1], 3);
+            L[1] = __builtin_amdgcn_alignbyte(L[1], L[0], 3);
+            L[0] = (L[0] << 8) | v;
+        };
 #pragma unroll 1
         for (int w = 0; w < 8; ++w) {
             uint32_t word = 0;
@@ -776,27 +784,34 @@ __global__ __launch_bounds__(FWG, 8) void rs_chien_k(const RsDevTables *__restri
             }
             if (w == 7)
                 word &= 0x7FFFFFFFu; /* i' = 255 repeats i' = 0 */
+            if (w == 0) {
+                z0 = word & 1u; /* i' = 0 is the reference's last point, i = 255 */
+                word &= ~1u;
+            }
             cnt += __popc(word);
-            if (fast)
-                rmap[w] = word;
+            const uint32_t wb = 32u * (uint32_t)w;
+            while (word != 0u) { /* at most deg <= 16 pushes per lane in all */
+                const uint32_t b = __builtin_ctz(word);
+                word &= word - 1u;
+                push(wb + b);
+            }
         }
+        if (z0)
+            push(255u);
+        cnt += z0;
         bool good = cnt == deg; /* src/decode.c:143-145 */
         if (P.pad > 0) {
             /* locations k = (i iprim - 1) mod 255 below pad fail, src/decode.c:132-134 */
-            uint32_t rb[8];
-#pragma unroll
-            for (int w = 0; w < 8; ++w)
-                rb[w] = fast ? rmap[w] : 0u;
-            RootIter it;
-            it.init(rb);
             bool low = false;
-            const uint32_t cmax = wave_max(good ? cnt : 0u);
-            for (uint32_t n = 0; n < cmax; ++n) {
-                const uint32_t i = it.next();
-                low |= n < cnt && (int32_t)((i * P.iprim + 254u) % 255u) < P.pad;
+#pragma unroll
+            for (int n = 0; n < 16; ++n) {
+                const uint32_t i = (L[n >> 2] >> (8 * (n & 3))) & 0xffu;
+                low |= (uint32_t)n < cnt && (int32_t)((i * P.iprim + 254u) % 255u) < P.pad;
             }
             good = good && !low;
         }
+        if (fast)
+            reinterpret_cast<uint4 *>(roots)[2 * cw] = make_uint4(L[0], L[1], L[2], L[3]);
         if (fast && !good) {
             {
                 ok[cw] = 0;
@@ -820,6 +835,7 @@ __global__ __launch_bounds__(FWG, 8) void rs_chien_k(const RsDevTables *__restri
  * FORNEY_R roots per step (their lookups issue together).  The locations and
  * magnitudes go out as a 32-byte record per codeword for rs_apply_k.
  */
+template <bool P11> /* fcr = 1 and prim = 1 (the default config): no multiplies for ln2 / locations */
 __global__ __launch_bounds__(FWG, FORNEY_WAVES) void rs_forney_k(const RsDevTables *__restrict__ T, RsCorrParams P,
                                                        uint8_t *data, size_t dstride, uint8_t *parity, size_t pstride,
                                                        size_t count, const uint8_t *__restrict__ lam,
@@ -833,6 +849,7 @@ __global__ __launch_bounds__(FWG, FORNEY_WAVES) void rs_forney_k(const RsDevTabl
     __syncthreads();
     const GfA gf{lds_addr(lgf) + 4u * (threadIdx.x & 31u) + 1u};
     const int32_t pad = P.pad;
+    constexpr bool fcr1 = P11, iprim1 = P11;
 
     for (size_t base = (size_t)blockIdx.x * FWG; base < count; base += (size_t)gridDim.x * FWG) {
         const size_t cw = base + threadIdx.x;
@@ -843,14 +860,12 @@ __global__ __launch_bounds__(FWG, FORNEY_WAVES) void rs_forney_k(const RsDevTabl
             continue;
         const uint32_t deg = fast ? (st & 31u) : 0u;
         uint4 o4 = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu), l4 = o4;
-        uint32_t rb[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        uint32_t rl[4] = {0, 0, 0, 0}; /* the root list (rs_chien_k), newest first; 0 past the last */
         if (fast) {
             o4 = reinterpret_cast<const uint4 *>(om)[cw];
             l4 = reinterpret_cast<const uint4 *>(lam)[cw];
-            const uint4 *r4 = reinterpret_cast<const uint4 *>(roots + cw * 32u);
-            const uint4 ra = r4[0], rc = r4[1];
-            rb[0] = ra.x, rb[1] = ra.y, rb[2] = ra.z, rb[3] = ra.w;
-            rb[4] = rc.x, rb[5] = rc.y, rb[6] = rc.z, rb[7] = rc.w;
+            const uint4 ra = reinterpret_cast<const uint4 *>(roots)[2 * cw];
+            rl[0] = ra.x, rl[1] = ra.y, rl[2] = ra.z, rl[3] = ra.w;
         }
         const uint32_t ow[4] = {o4.x, o4.y, o4.z, o4.w}, lw[4] = {l4.x, l4.y, l4.z, l4.w};
         /* address-form logs: Omega_m packed two per register, and the
@@ -875,8 +890,6 @@ __global__ __launch_bounds__(FWG, FORNEY_WAVES) void rs_forney_k(const RsDevTabl
 #define LODD(h) (((h) & 1) ? (lod[(h) >> 1] >> 16) : (lod[(h) >> 1] & 0xffffu))
         const uint32_t degmax = wave_max(deg);
         const uint32_t nir = max(degmax, wave_max(dtop) + 1u); /* powers i m needed: m < nir */
-        RootIter it;
-        it.init(rb);
         /* phase 1: every root's location byte and magnitude, packed four per
          * register (the roots' loop is unrolled: FORNEY_R per step, steps past
          * the wave's degree skipped) */
@@ -889,7 +902,7 @@ __global__ __launch_bounds__(FWG, FORNEY_WAVES) void rs_forney_k(const RsDevTabl
             uint32_t ir[FORNEY_R];
 #pragma unroll
             for (int t = 0; t < FORNEY_R; ++t)
-                ir[t] = it.next(); /* 255 past the last root */
+                ir[t] = (rl[(n + t) >> 2] >> (8 * ((n + t) & 3))) & 0xffu; /* any order: roots are independent */
             /* powers alpha^(i m) as plain scaled logs 128 (i m mod 255), even
              * and odd m in two chains */
             uint32_t i2[FORNEY_R], ie[FORNEY_R], io[FORNEY_R], nm[FORNEY_R], den[FORNEY_R];
@@ -922,12 +935,18 @@ __global__ __launch_bounds__(FWG, FORNEY_WAVES) void rs_forney_k(const RsDevTabl
             }
 #pragma unroll
             for (int t = 0; t < FORNEY_R; ++t) {
-                const uint32_t ln2 = mod255((uint32_t)((int32_t)ir[t] * ((int32_t)P.fcr - 1) + (int32_t)RS_NN));
+                /* fcr = 1 (the default config): alpha^(i (fcr - 1)) = 1, log 0 */
+                const uint32_t ln2 =
+                    fcr1 ? 0u : mod255((uint32_t)((int32_t)ir[t] * ((int32_t)P.fcr - 1) + (int32_t)RS_NN));
                 const uint32_t lden = gf.plog(gf.loga(den[t])); /* log 0 = 255 in the reference: no den = 0 guard */
-                const uint32_t lm = (gf.plog(gf.loga(nm[t])) + ln2 + RS_NN - lden) % 255u;
+                /* (log num + ln2 + 255 - log den) mod 255 -- sum < 765, one
+                 * reduction leaves it < 510, inside the exp table's two periods */
+                const uint32_t lm = red(gf.plog(gf.loga(nm[t])) + ln2 + RS_NN - lden);
                 const bool z = (uint32_t)(n + t) < deg && nm[t] != 0u; /* zero numerator: no correction, not counted */
                 fixed += z ? 1u : 0u;
-                const uint32_t p = (uint32_t)((int32_t)((ir[t] * P.iprim + 254u) % 255u) - pad); /* < size + 32 */
+                /* location k = (i iprim - 1) mod 255 (i = 1..255); iprim = 1: i - 1 */
+                const uint32_t k = iprim1 ? ir[t] - 1u : (ir[t] * P.iprim + 254u) % 255u;
+                const uint32_t p = (uint32_t)((int32_t)k - pad); /* < size + 32 */
                 posp[(n + t) >> 2] |= p << (8 * ((n + t) & 3));
                 magp[(n + t) >> 2] |= (z ? gf.exp(lm) : 0u) << (8 * ((n + t) & 3));
             }
@@ -1077,8 +1096,12 @@ extern "C" hipError_t rsk_forney(const RsDevTables *tab, const RsCorrParams *prm
 {
     if (count == 0)
         return hipSuccess;
-    hipLaunchKernelGGL(rs_forney_k, dim3(fast_grid(count, num_cu)), dim3(FWG), 0, stream, tab, *prm, data, dstride,
-                       parity, pstride, count, ws->lam, ws->om, ws->roots, ws->meta, ok, corrected);
+    if (prm->fcr == 1u && prm->iprim == 1u)
+        hipLaunchKernelGGL(rs_forney_k<true>, dim3(fast_grid(count, num_cu)), dim3(FWG), 0, stream, tab, *prm, data,
+                           dstride, parity, pstride, count, ws->lam, ws->om, ws->roots, ws->meta, ok, corrected);
+    else
+        hipLaunchKernelGGL(rs_forney_k<false>, dim3(fast_grid(count, num_cu)), dim3(FWG), 0, stream, tab, *prm, data,
+                           dstride, parity, pstride, count, ws->lam, ws->om, ws->roots, ws->meta, ok, corrected);
     return hipGetLastError();
 }
 
