@@ -49,6 +49,9 @@ typedef __attribute__((address_space(1))) const uint32_t gu32;
 #define LFSR_STAGGER 0 /* (experiment) odd waves sleep LFSR_STAGGER x 8128 cycles first */
 #endif
 #define LFSR_REPL 16
+#ifndef LFSR_USTORE
+#define LFSR_USTORE 1
+#endif
 
 /* ------------------------------------------------------------------------ */
 /* LFSR (encode / syndromes / check)                                        */
@@ -391,7 +394,16 @@ __device__ __forceinline__ void lfsr_epilogue(const uint32_t (&P)[8], const uint
     } else if (MODE == MODE_CHECK) {
         out[cw] = (P[0] | P[1] | P[2] | P[3] | P[4] | P[5] | P[6] | P[7]) != 0u;
     } else {
+#if LFSR_USTORE /* two unaligned 16-byte stores (gfx950 supports them, tools/probes/unaligned.hip) */
+        typedef unsigned u32x4s __attribute__((ext_vector_type(4), aligned(1)));
+        typedef __attribute__((address_space(1))) u32x4s gu32x4s;
+        gu32x4s *o = (gu32x4s *)(uintptr_t)(parity + cw * pstride);
+        const u32x4s a = {P[0], P[1], P[2], P[3]}, b = {P[4], P[5], P[6], P[7]};
+        o[0] = a;
+        o[1] = b;
+#else
         store32_any(parity + cw * pstride, P);
+#endif
     }
 }
 
