@@ -489,6 +489,12 @@ static void build_tables(poporon_t *h)
             const uint32_t la = x < 256u ? (x ? (uint32_t)t.log[x] * 128u + 4u * r + 1u : 128u * RS_Z0 + 4u * r) : 0u;
             gfa[x * 32 + r] = ((uint32_t)t.exp2[x] << 8) | (la << 16);
         }
+    uint32_t *gfc = reinterpret_cast<uint32_t *>(t.gfc);
+    for (uint32_t x = 0; x < 512; x++)
+        for (uint32_t r = 0; r < 32; r++) {
+            const uint32_t v = x & 255u;
+            gfc[x * 32 + r] = ((uint32_t)t.exp2[x] << 8) | ((v ? (uint32_t)t.log[v] * 128u : 0xFFFFu) << 16);
+        }
     const char *fv = getenv("POPORON_AMD_FORCE_VERIFY");
     p.force_verify = (fv && fv[0] == '1') ? 1u : 0u;
     const char *sa = getenv("POPORON_AMD_STOP_AT"); /* profiling ablation only */

@@ -669,14 +669,26 @@ __global__ __launch_bounds__(COR_WG) void rs_correct_k(const RsDevTables *__rest
     uint8_t *lsyn = reinterpret_cast<uint8_t *>(lds) + LDS_SYN;
     uint4 *lch = lds + LDS_CH / 16;
     uint32_t *lgf = reinterpret_cast<uint32_t *>(reinterpret_cast<uint8_t *>(lds) + LDS_GF);
-    for (uint32_t t = threadIdx.x; t < 512u * GF_REPL; t += COR_WG) {
-        const uint32_t x = t / GF_REPL;
-        const uint32_t v = x & 255u;
-        /* byte 1: exp2[x]; bytes 2-3: scaled log of x & 255 (0xFFFF for 0) */
-        lgf[t] = ((uint32_t)T->exp2[x] << 8) | ((v ? (uint32_t)T->log[v] * 128u : 0xFFFFu) << 16);
+    {
+        /* byte 1: exp2[x]; bytes 2-3: scaled log of x & 255 (0xFFFF for 0):
+         * the host-built image RsDevTables::gfc, and the Chien rows -- every
+         * load issued before the first store (a rolled loop waits for each) */
+        static_assert(GF_REPL == 32, "gfc is built for 32 replicas");
+        constexpr int KG = 512 * GF_REPL / 4 / COR_WG, KC = 16 * 256 / COR_WG;
+        uint4 g[KG], c[KC];
+#pragma unroll
+        for (int k = 0; k < KG; ++k)
+            g[k] = T->gfc[threadIdx.x + k * COR_WG];
+#pragma unroll
+        for (int k = 0; k < KC; ++k)
+            c[k] = T->chien[threadIdx.x + k * COR_WG];
+#pragma unroll
+        for (int k = 0; k < KG; ++k)
+            reinterpret_cast<uint4 *>(lgf)[threadIdx.x + k * COR_WG] = g[k];
+#pragma unroll
+        for (int k = 0; k < KC; ++k)
+            lch[threadIdx.x + k * COR_WG] = c[k];
     }
-    for (uint32_t t = threadIdx.x; t < 16u * 256u; t += COR_WG)
-        lch[t] = T->chien[t];
     __syncthreads();
     const Gf gf{lds_addr(lgf) + (threadIdx.x & (GF_REPL - 1)) * 4 + 1};
     uint8_t *srow = lsyn + threadIdx.x;

@@ -50,6 +50,10 @@ struct RsDevTables {
      *   128 RS_Z0 + 4r for x = 0, 0 for x >= 256
      * (copied into LDS at address 0 by every workgroup: 4 uint4 per thread) */
     uint4 gfa[512 * 32 / 4];
+    /* gfc: the LDS image of the general correction kernel's GF table
+     * (rs_correct.hip), dword x * 32 + r: (exp2[x] << 8) | (s << 16) with s =
+     * 128 log (x & 255), 0xFFFF for x & 255 = 0 */
+    uint4 gfc[512 * 32 / 4];
 };
 #define RS_Z0 200u /* zero sentinel row of gfa (rs_fast.hip) */
 
