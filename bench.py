@@ -65,6 +65,8 @@ M64 = (1 << 64) - 1
 def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--overlap", type=int, default=0,
+                    help="1: each step's encode on a second stream, concurrent with its decode")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=1 << 20, help="codewords per GPU (weak-scaling line)")
@@ -202,9 +204,17 @@ class GpuBackend:
         pos, mag = err
         self.T.channel_xor(pos.data_ptr(), mag.data_ptr(), pos.shape[1], buf.data_ptr(), N, buf.shape[0], self.stream)
 
-    def encode(self, buf):
+    def encode(self, buf, side=False):
+        """side=True: on a second stream (the caller orders it: the step's
+        encode and decode touch different buffers and may run concurrently)"""
         b = buf.data_ptr()
-        self.rs.encode_batch_device(b, N, b + K, N, K, buf.shape[0], self.stream)
+        s = self.stream
+        if side:
+            if getattr(self, "side_stream", None) is None:
+                self.side = self.torch.cuda.Stream(device=self.dev)
+                self.side_stream = self.side.cuda_stream
+            s = self.side_stream
+        self.rs.encode_batch_device(b, N, b + K, N, K, buf.shape[0], s)
 
     def status(self, n):
         return (self.torch.zeros(n, dtype=self.torch.uint8, device=self.dev),
@@ -320,7 +330,9 @@ def run_weak(be, ranks, args, rank, world):
         be.sync()
 
     def step(k):
-        be.encode(cw)
+        # the step's encode (messages in cw) and decode (a corrupted copy)
+        # share no buffer: with --overlap the encode goes to a second stream
+        be.encode(cw, side=args.overlap and copies and be.kind == "gpu")
         if copies:
             d = bad[k]
         else:

@@ -45,7 +45,7 @@ class Backend:
         pos, mag = err
         buf[...] = T.channel_xor_cpu(buf, pos, mag)
 
-    def encode(self, buf):
+    def encode(self, buf, side=False):
         buf[:, K:] = self.o.encode_batch(np.ascontiguousarray(buf[:, :K]))
 
     def status(self, n):
