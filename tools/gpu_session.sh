@@ -27,7 +27,7 @@ for step in "$@"; do
     tests_all) run tests_all 900 python -m pytest tests -m gpu -q ;;
     bench) run bench 600 python bench.py ;;
     prof) run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- \
-        python3 bench.py --no-cpu-baseline --no-host --steps 10 ;;
+        python3 bench.py --no-cpu-baseline --no-host --no-c4 --no-erasure --no-latency --steps 10 ;;
     pmc)
         # one rocprofv3 pass per counter group (never combined with tracing)
         i=0
