@@ -61,9 +61,6 @@
 #ifndef FORNEY_WAVES
 #define FORNEY_WAVES 8
 #endif
-#ifndef BM_SWAR
-#define BM_SWAR 0     /* 1: packed BM (v_perm products, carried discrepancies); 0: log-form lookups */
-#endif
 #ifndef APPLY_REV
 #define APPLY_REV 1
 #endif
@@ -141,190 +138,6 @@ static int fast_grid(size_t count, int num_cu)
  * i of iteration r = 4q+1+s reads entry 3 - s + i at a compile-time place
  * (the four iterations are unrolled; blocks are a rolled loop).
  */
-#if BM_SWAR
-/*
- * Packed (SWAR) form.  All polynomials are kept as bytes, four coefficients to
- * a register, and every product in the iteration is one scalar q = disc / b
- * times a packed polynomial.  Multiplication by a fixed q is GF(2)-linear in
- * the bits of the other operand, x q = T0[x & 7] ^ T1[(x >> 3) & 7] ^
- * T2[x >> 6], and v_perm_b32 looks up four bytes at once in an 8-byte table:
- * 10 VALU per four products and no LDS (the tables are built from the eight
- * bytes q alpha^k, k = 0..7: eight LDS reads per iteration).
- *
- * The discrepancies are not dot products: Delta(x) = Lambda(x) S(x) mod x^32
- * is carried along (Sarwate-Shanbhag's reformulation), so that discrepancy r
- * is the byte Delta_(r-1).  With C = x B and Psi = C S, one iteration is
- *   Lambda ^= q C,  Delta ^= q Psi,
- *   C <- x Lambda_old, Psi <- x Delta_old  (lengthening)  or  C <- x C, Psi <- x Psi.
- * Delta is exact whatever the cut at x^16 does to Lambda (Psi is never cut),
- * and at the end Omega = Delta mod x^deg (src/decode.c:147-158) comes free.
- * The iteration count is a compile-time constant (fully unrolled), so every
- * byte position is an immediate and dwords of Delta / Psi no later
- * discrepancy reads (Delta_k for k >= 16 is last read at iteration k + 1)
- * are dropped.  The same products as the reference's Karn form: rs_correct.hip
- * shows Massey's unnormalised form equal to it, and this is that form.
- */
-struct QMul {
-    uint32_t t0l, t0h, t1l, t1h, t2;
-    /* the tables of q from a_k = q alpha^k */
-    __device__ __forceinline__ void build(const uint32_t (&a)[8])
-    {
-        t0l = (a[0] << 8) | (a[1] << 16) | ((a[0] ^ a[1]) << 24);
-        t0h = t0l ^ (a[2] * 0x01010101u);
-        t1l = (a[3] << 8) | (a[4] << 16) | ((a[3] ^ a[4]) << 24);
-        t1h = t1l ^ (a[5] * 0x01010101u);
-        t2 = (a[6] << 8) | (a[7] << 16) | ((a[6] ^ a[7]) << 24);
-    }
-    /* q times each byte of x */
-    __device__ __forceinline__ uint32_t mul(uint32_t x) const
-    {
-        const uint32_t p0 = __builtin_amdgcn_perm(t0h, t0l, x & 0x07070707u);
-        const uint32_t p1 = __builtin_amdgcn_perm(t1h, t1l, (x >> 3) & 0x07070707u);
-        const uint32_t p2 = __builtin_amdgcn_perm(t2, t2, (x >> 6) & 0x03030303u);
-        return xor3(p0, p1, p2);
-    }
-};
-
-__device__ __forceinline__ uint32_t byte_of(const uint32_t *v, int i) { return (v[i >> 2] >> (8 * (i & 3))) & 0xffu; }
-
-
-__global__ __launch_bounds__(FWG, BM_WAVES) void rs_bm_k(const RsDevTables *__restrict__ T, const uint8_t *__restrict__ syn,
-                                                   size_t count, uint8_t *__restrict__ lamo, uint8_t *__restrict__ omo,
-                                                   uint8_t *__restrict__ meta, uint32_t *__restrict__ list,
-                                                   uint32_t *__restrict__ nlist, uint8_t *__restrict__ ok,
-                                                   uint8_t *__restrict__ corrected)
-{
-    __shared__ uint32_t lgf[512 * 32];
-    fill_gfa(lgf, T);
-    __syncthreads();
-    const GfA gf{lds_addr(lgf) + 4u * (threadIdx.x & 31u) + 1u};
-    const uint32_t pofs = gf.pofs;
-
-    for (size_t base = (size_t)blockIdx.x * FWG; base < count; base += (size_t)gridDim.x * FWG) {
-        const size_t cw = base + threadIdx.x;
-        const bool valid = cw < count;
-        uint4 sa = make_uint4(0, 0, 0, 0), sb = sa;
-        if (valid) {
-            const uint4 *sp = reinterpret_cast<const uint4 *>(syn + cw * RS_NR);
-            sa = sp[0];
-            sb = sp[1];
-        }
-        const bool any = (sa.x | sa.y | sa.z | sa.w | sb.x | sb.y | sb.z | sb.w) != 0u;
-        if (__ballot(any) == 0ull) { /* uniform: every codeword of the wave is clean */
-            if (valid) {
-                ok[cw] = 1;
-                if (corrected)
-                    corrected[cw] = 0;
-                meta[cw] = (uint8_t)(RS_ST_DONE << 5);
-            }
-            continue;
-        }
-        /* Lambda_0..19 (only 0..16 kept), C = x B (bytes 0..19; byte 17 = B_16),
-         * Delta = Lambda S and Psi = C S mod x^32 */
-        uint32_t lm[5] = {1u, 0u, 0u, 0u, 0u}, cc[5] = {0x100u, 0u, 0u, 0u, 0u};
-        uint32_t dl[8] = {sa.x, sa.y, sa.z, sa.w, sb.x, sb.y, sb.z, sb.w}, ps[8];
-        ps[0] = dl[0] << 8;
-#pragma unroll
-        for (int j = 1; j < 8; ++j)
-            ps[j] = __builtin_amdgcn_alignbyte(dl[j], dl[j - 1], 3);
-        uint32_t L = 0, lb = 0, over = 0, bo = 0; /* over, bo: 0 / 1 */
-
-        static_for<1, RS_NR + 1, 1>([&](auto rc) __attribute__((always_inline)) {
-            constexpr int r = decltype(rc)::value;
-            const uint32_t disc = byte_of(dl, r - 1);
-            const uint32_t ld = gf.logs(disc);
-            const bool upd = disc != 0u;
-            const bool lengthen = upd && (2u * L <= (uint32_t)(r - 1));
-            const int32_t dd = (int32_t)ld - (int32_t)lb;
-            const uint32_t dq = upd ? (uint32_t)(dd < 0 ? dd + 255 * 128 : dd) : SZ; /* scaled log q (zero: SZ) */
-            const uint32_t b16 = ((cc[4] >> 8) & 0xffu) != 0u;
-            over |= upd ? (bo | b16) : 0u;     /* Lambda would get a term past x^16 */
-            bo = lengthen ? 0u : (bo | b16);  /* C <- x C pushes B_16 past the cut */
-            /* a_k = q alpha^k: immediate offsets of one address (zero q reads zeros) */
-            uint32_t a[8];
-#pragma unroll
-            for (int k = 0; k < 8; ++k)
-                a[k] = lds8(pofs + dq + 128u * (uint32_t)k);
-            QMul q;
-            q.build(a);
-            /* Lambda ^= q C, C <- x (Lambda_old or C); dwords of C above x^r are zero */
-            /* before this iteration deg C <= r and deg Lambda < r: dwords past
-             * NC are zero and stay so; dword NC only receives the shift */
-            constexpr int NC = (r >> 2) + 1 < 4 ? (r >> 2) + 1 : 4;
-#pragma unroll
-            for (int k = NC; k >= 0; --k) {
-                const uint32_t sk = lengthen ? lm[k] : cc[k];
-                const uint32_t sk1 = k > 0 ? (lengthen ? lm[k - 1] : cc[k - 1]) : 0u;
-                if (4 * k <= r)
-                    lm[k] ^= q.mul(cc[k]);
-                cc[k] = k > 0 ? __builtin_amdgcn_alignbyte(sk, sk1, 3) : (sk << 8);
-            }
-            /* Delta ^= q Psi on the dwords still read (0..3 for Omega, the
-             * rest while a later discrepancy lies in them); Psi shifted likewise */
-#pragma unroll
-            for (int j = 7; j >= 0; --j) {
-                if (j >= 4 && r > 4 * j + 3)
-                    continue;
-                const uint32_t sj = lengthen ? dl[j] : ps[j];
-                const uint32_t sj1 = j > 0 ? (lengthen ? dl[j - 1] : ps[j - 1]) : 0u;
-                const uint32_t t = q.mul(ps[j]);
-                dl[j] ^= t;
-                ps[j] = j > 0 ? __builtin_amdgcn_alignbyte(sj, sj1, 3) : (sj << 8);
-            }
-            if (lengthen) {
-                L = (uint32_t)r - L;
-                lb = ld;
-            }
-            /* one iteration at a time: the state is pinned at the end of
-             * every iteration (otherwise the compiler sinks products it can
-             * defer, keeping eight tables live, and hoists index extractions
-             * -- both spill) */
-#pragma unroll
-            for (int k = 0; k < 5; ++k)
-                asm volatile("" : "+v"(lm[k]), "+v"(cc[k]));
-            asm volatile("" : "+v"(over), "+v"(bo), "+v"(L), "+v"(lb));
-#pragma unroll
-            for (int j = 0; j < 8; ++j)
-                if (j < 4 || r <= 4 * j + 2)
-                    asm volatile("" : "+v"(dl[j]), "+v"(ps[j]));
-            __builtin_amdgcn_sched_barrier(0);
-        });
-
-        /* ---- degree, src/decode.c:98-110 ---- */
-        uint32_t deg = 0;
-#pragma unroll
-        for (int i = 1; i < NL; ++i)
-            deg = byte_of(lm, i) ? (uint32_t)i : deg;
-        const bool fast = any && !over && deg == L && deg != 0u;
-
-        if (valid) {
-            if (!any) {
-                ok[cw] = 1;
-                if (corrected)
-                    corrected[cw] = 0;
-                meta[cw] = (uint8_t)(RS_ST_DONE << 5);
-            } else if (!fast) {
-                meta[cw] = (uint8_t)(RS_ST_LIST << 5);
-                list[atomicAdd(nlist, 1u)] = (uint32_t)cw;
-            } else {
-                /* logs of Lambda_1..16 and of Omega_0..deg-1 (255: zero / past deg) */
-                uint32_t lb4[4] = {0, 0, 0, 0}, ob[4] = {0, 0, 0, 0};
-#pragma unroll
-                for (int j = 1; j < NL; ++j)
-                    lb4[(j - 1) >> 2] |= gf.plog(gf.loga(byte_of(lm, j))) << (8 * ((j - 1) & 3));
-#pragma unroll
-                for (int m = 0; m < 16; ++m) {
-                    const uint32_t o = (uint32_t)m < deg ? gf.plog(gf.loga(byte_of(dl, m))) : 255u;
-                    ob[m >> 2] |= o << (8 * (m & 3));
-                }
-                reinterpret_cast<uint4 *>(lamo)[cw] = make_uint4(lb4[0], lb4[1], lb4[2], lb4[3]);
-                reinterpret_cast<uint4 *>(omo)[cw] = make_uint4(ob[0], ob[1], ob[2], ob[3]);
-                meta[cw] = (uint8_t)((RS_ST_FAST << 5) | deg);
-            }
-        }
-    }
-}
-#else
 __global__ __launch_bounds__(FWG, BM_WAVES) void rs_bm_k(const RsDevTables *__restrict__ T, const uint8_t *__restrict__ syn,
                                                    size_t count, uint8_t *__restrict__ lamo, uint8_t *__restrict__ omo,
                                                    uint8_t *__restrict__ meta, uint32_t *__restrict__ list,
@@ -520,7 +333,6 @@ __global__ __launch_bounds__(FWG, BM_WAVES) void rs_bm_k(const RsDevTables *__re
     }
 }
 
-#endif /* BM_SWAR */
 
 /* ------------------------------------------------------------------------ */
 /* rs_bm16_k: the north_star mapping -- sixteen lanes per codeword          */
