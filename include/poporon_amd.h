@@ -129,7 +129,9 @@ bool poporon_decode_batch(poporon_t *pprn, uint8_t *data, size_t data_stride, ui
  * 0 = encode LFSR, 1 = remainder LFSR, 2 = correction (single kernel),
  * 3 = check LFSR; the split error-mode decode of large batches: 4 = BM +
  * Omega, 5 = Chien, 6 = Forney, 8 = apply, 7 = the general kernel over the
- * codewords the split kernels hand on.
+ * codewords the split kernels hand on.  Erasure-mode batches of that size:
+ * 1, 9 = the locator / Omega / Forney kernel for 32 sorted erasures (prim 1),
+ * 7 = the general kernel over the rest (records), 8 = apply.
  *
  * Error-mode batches of at least 8192 codewords (no erasures, no external
  * syndromes) take the split decode; POPORON_AMD_DECODE_PATH=split / single
@@ -143,6 +145,7 @@ bool poporon_decode_batch(poporon_t *pprn, uint8_t *data, size_t data_stride, ui
 #define POPORON_AMD_KERNEL_FORNEY 6
 #define POPORON_AMD_KERNEL_LIST 7
 #define POPORON_AMD_KERNEL_APPLY 8
+#define POPORON_AMD_KERNEL_ERASURE 9
 bool poporon_amd_timing(poporon_t *pprn, int enable);
 bool poporon_amd_timing_read(poporon_t *pprn, int kernel, double *total_ms, uint64_t *launches);
 

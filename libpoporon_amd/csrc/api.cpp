@@ -105,7 +105,7 @@ struct _poporon_config_t {
     uint8_t correction_capability; /* BCH */
 };
 
-#define NKERN 9
+#define NKERN 10
 struct TimedLaunch {
     int kernel;
     hipEvent_t a, b;
@@ -1170,6 +1170,53 @@ static bool launch_decode(poporon_t *h, uint8_t *d_data, size_t ds, uint8_t *d_p
             return false;
         return !shared || rem_release(g, s);
     }
+    /* erasure batches: the general kernel's decode with the corrections as
+     * records, applied block-wise (scattered byte read-modify-writes cost
+     * ~0.3 ms per 2^20 codewords with 32 erasures) */
+    const bool esplit = !ext_syn && (pos8 || pos32) && prm.vfast && !prm.force_verify && !prm.stop_at &&
+                        h->decode_path != 2 && (h->decode_path == 1 || count >= SPLIT_MIN_COUNT);
+    if (esplit) {
+        const RsSplitWs ws = rs_ws_carve(rem, rem_cap ? rem_cap : count);
+        GpuCtx &g = h->gpu;
+        /* 32 sorted erasures (prim 1): rs_era_k, the rest through the list */
+        const bool efast = pos8 && prm.prim == 1u && pos_stride % 16u == 0u &&
+                           (reinterpret_cast<uintptr_t>(pos8) & 15u) == 0u;
+        if (efast) {
+            {
+                KernelTimer t(g, POPORON_AMD_KERNEL_REMAINDER, s);
+                HIP_OK(rsk_syndrome_reset(g.tab, d_data, ds, d_par, ps, (uint32_t)size, count, ws.syn, ws.nlist,
+                                          g.num_cu, s));
+                t.done();
+            }
+            {
+                KernelTimer t(g, POPORON_AMD_KERNEL_ERASURE, s);
+                HIP_OK(rsk_era(g.tab, &prm, &ws, pos8, pos_stride, cnt, count, ok, corrected, g.num_cu, s));
+                t.done();
+            }
+            {
+                KernelTimer t(g, POPORON_AMD_KERNEL_LIST, s);
+                HIP_OK(rsk_correct_era_list(g.tab, &prm, count, ws.syn, pos8, pos_stride, cnt, ok, corrected, ws.lam,
+                                            ws.meta, ws.list, ws.nlist, g.num_cu, s));
+                t.done();
+            }
+        } else {
+            {
+                KernelTimer t(g, POPORON_AMD_KERNEL_REMAINDER, s);
+                HIP_OK(rsk_syndrome(g.tab, d_data, ds, d_par, ps, (uint32_t)size, count, ws.syn, g.num_cu, s));
+                t.done();
+            }
+            KernelTimer t(g, POPORON_AMD_KERNEL_CORRECT, s);
+            HIP_OK(rsk_correct_era_rec(g.tab, &prm, count, ws.syn, pos8, pos32, pos_stride, cnt, ok, corrected, ws.lam,
+                                       ws.meta, g.num_cu, s));
+            t.done();
+        }
+        {
+            KernelTimer t(g, POPORON_AMD_KERNEL_APPLY, s);
+            HIP_OK(rsk_apply_era(&prm, ws.meta, ws.lam, d_data, ds, d_par, ps, count, s));
+            t.done();
+        }
+        return !shared || rem_release(g, s);
+    }
     if (!ext_syn) {
         KernelTimer t(h->gpu, POPORON_AMD_KERNEL_REMAINDER, s);
         HIP_OK(rsk_syndrome(h->gpu.tab, d_data, ds, d_par, ps, (uint32_t)size, count, rem, h->gpu.num_cu, s));
@@ -1449,7 +1496,7 @@ EXPORT bool poporon_decode_batch(poporon_t *h, uint8_t *data, size_t data_stride
     /* parity right after the data in rows of equal stride: move whole rows */
     const bool rows = parity == data + size && parity_stride == data_stride;
     for (auto &ps : g.pipe)
-        if (!pipe_slot(h, ps, chunk * per + 256 + rs_ws_bytes(chunk)))
+        if (!pipe_slot(h, ps, chunk * per + 512 + rs_ws_bytes(chunk)))
             return false;
     auto finish = [&](GpuCtx::PipeSlot &ps) -> bool {
         if (!ps.busy)
@@ -1476,7 +1523,9 @@ EXPORT bool poporon_decode_batch(poporon_t *h, uint8_t *data, size_t data_stride
             break;
         const size_t n = std::min(chunk, count - c0);
         uint8_t *hc = ps.host, *dc = ps.dev;
-        const size_t o_ok = n * w, o_cor = o_ok + n, o_pos = o_cor + n, o_cnt = o_pos + (positions ? n * nr : 0);
+        /* positions 16-byte aligned: the 32-erasure kernel reads them as uint4 */
+        const size_t o_ok = n * w, o_cor = o_ok + n, o_pos = (o_cor + n + 15) & ~(size_t)15,
+                     o_cnt = o_pos + (positions ? n * nr : 0);
         const size_t o_rem = (o_cnt + (positions ? n : 0) + 255) & ~(size_t)255;
         /* codeword rows [data | parity] */
         if (rows) {

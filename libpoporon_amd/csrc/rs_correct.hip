@@ -87,10 +87,10 @@ struct Gf {
     __device__ __forceinline__ uint32_t pofs() const { return pa; }
 };
 
-template <typename PosT, bool ERA>
+template <typename PosT, bool ERA, bool REC>
 __device__ __forceinline__ bool correct_one(const Gf &gf, const uint4 *__restrict__ chien, const uint8_t *srow,
                                             const RsCorrParams &P, uint8_t *data, uint8_t *parity, uint32_t ne,
-                                            const PosT *pos, uint32_t &corrected)
+                                            const PosT *pos, uint8_t *recp, uint32_t &corrected)
 {
     const int32_t pad = P.pad;
     const uint32_t size = P.size;
@@ -499,7 +499,56 @@ __device__ __forceinline__ bool correct_one(const Gf &gf, const uint4 *__restric
         auto target = [&](uint32_t p) __attribute__((always_inline)) {
             return p < size ? data + p : (p < size + RS_NR ? parity + (p - size) : data);
         };
-        if (pass == 1u) {
+        if (pass == 1u && REC) {
+            if constexpr (ERA && REC) {
+                /* record mode (the split erasure decode): the magnitudes go to
+                 * this codeword's 64-byte record -- 32 slot positions (clamped
+                 * to 255), 32 magnitudes (0: nothing to apply) -- and rs_apply_k
+                 * XORs them in (a zero numerator corrects nothing and is not
+                 * counted; repeated slots accumulate as in the reference) */
+                static_assert(FORNEY_R == 4, "record words hold four magnitudes");
+                uint32_t pk[RS_NR / 4], M[RS_NR / 4];
+#pragma unroll
+                for (int q = 0; q < RS_NR / 4; ++q) {
+                    pk[q] = 0;
+                    M[q] = 0;
+                }
+#pragma unroll
+                for (int n = 0; n < RS_NR; ++n) {
+                    const uint32_t p = (uint32_t)n < cnt ? min((uint32_t)pos[n], 255u) : 255u;
+                    pk[n >> 2] |= p << (8 * (n & 3));
+                }
+                uint32_t steps = 0;
+                for (uint32_t n = 0; n < cntmax; n += FORNEY_R) {
+                    uint32_t cur = 0;
+#pragma unroll
+                    for (int t = 0; t < FORNEY_R; ++t) {
+                        uint32_t lm;
+                        const uint32_t num = forney(it.next(), lm);
+                        const bool z = n + t < cnt && num != 0u;
+                        if (!verify)
+                            corrected += z ? 1u : 0u;
+                        cur |= (z ? gf.exp(lm) : 0u) << (8 * t);
+                    }
+#pragma unroll
+                    for (int q = 0; q < RS_NR / 4 - 1; ++q)
+                        M[q] = M[q + 1];
+                    M[RS_NR / 4 - 1] = cur;
+                    ++steps;
+                }
+                for (; steps < RS_NR / 4; ++steps) { /* uniform: words into place */
+#pragma unroll
+                    for (int q = 0; q < RS_NR / 4 - 1; ++q)
+                        M[q] = M[q + 1];
+                    M[RS_NR / 4 - 1] = 0;
+                }
+                uint4 *r = reinterpret_cast<uint4 *>(recp);
+                r[0] = make_uint4(pk[0], pk[1], pk[2], pk[3]);
+                r[1] = make_uint4(pk[4], pk[5], pk[6], pk[7]);
+                r[2] = make_uint4(M[0], M[1], M[2], M[3]);
+                r[3] = make_uint4(M[4], M[5], M[6], M[7]);
+            }
+        } else if (pass == 1u) {
             /* apply (src/decode.c:211-227), FORNEY_R roots per step: their
              * sums are independent (the lookups of a step issue together),
              * and the bytes they correct are loaded one step ahead, so the
@@ -646,7 +695,9 @@ __device__ __forceinline__ bool correct_one(const Gf &gf, const uint4 *__restric
     return good;
 }
 
-template <typename PosT, bool ERA>
+/* REC (erasure mode): corrections go to 64-byte records (rec) for rs_apply_k,
+ * meta[cw] = RS_ST_FAST where a record was written, RS_ST_DONE elsewhere */
+template <typename PosT, bool ERA, bool REC = false>
 __global__ __launch_bounds__(COR_WG) void rs_correct_k(const RsDevTables *__restrict__ T, RsCorrParams P,
                                                        uint8_t *data, size_t dstride, uint8_t *parity, size_t pstride,
                                                        size_t count, const uint8_t *__restrict__ syn,
@@ -655,7 +706,9 @@ __global__ __launch_bounds__(COR_WG) void rs_correct_k(const RsDevTables *__rest
                                                        const uint8_t *__restrict__ cnt, uint8_t *__restrict__ ok,
                                                        uint8_t *__restrict__ corrected,
                                                        const uint32_t *__restrict__ list,
-                                                       const uint32_t *__restrict__ list_n)
+                                                       const uint32_t *__restrict__ list_n,
+                                                       uint8_t *__restrict__ rec = nullptr,
+                                                       uint8_t *__restrict__ meta = nullptr)
 {
     /* list mode (the split decode's fallback, rs_fast.hip): the codewords
      * list[0 .. *list_n); otherwise 0 .. count - 1.  Blocks with no work
@@ -733,14 +786,17 @@ __global__ __launch_bounds__(COR_WG) void rs_correct_k(const RsDevTables *__rest
         uint32_t fixed = 0;
         bool good = !refuse;
         if (__ballot(need) != 0ull) { /* uniform: the whole wave enters */
-            const bool r = correct_one<PosT, ERA>(gf, lch, srow, P, data + cs * dstride, parity + cs * pstride,
-                                                  need ? ne0 : 0u, ERA ? pos + cs * pos_stride : nullptr, fixed);
+            const bool r = correct_one<PosT, ERA, REC>(gf, lch, srow, P, data + cs * dstride, parity + cs * pstride,
+                                                       need ? ne0 : 0u, ERA ? pos + cs * pos_stride : nullptr,
+                                                       REC ? rec + cs * 64u : nullptr, fixed);
             good = need ? r : good;
         }
         if (valid) {
             ok[cw] = good ? 1 : 0;
             if (corrected)
                 corrected[cw] = (uint8_t)fixed;
+            if constexpr (REC)
+                meta[cw] = (uint8_t)(((need && good) ? RS_ST_FAST : RS_ST_DONE) << 5);
         }
     }
 }
@@ -787,5 +843,43 @@ extern "C" hipError_t rsk_correct_list(const RsDevTables *tab, const RsCorrParam
     const dim3 grid(std::min(persistent_grid(count, COR_WG, num_cu), 64));
     hipLaunchKernelGGL((rs_correct_k<uint8_t, false>), grid, dim3(COR_WG), 0, stream, tab, *prm, data, dstride,
                        parity, pstride, count, syn, nullptr, 0, nullptr, 0, nullptr, ok, corrected, list, list_n);
+    return hipGetLastError();
+}
+
+/* erasure mode with the corrections as records (the split erasure decode,
+ * then rsk_apply_era): rec 64 B and meta 1 B per codeword */
+extern "C" hipError_t rsk_correct_era_rec(const RsDevTables *tab, const RsCorrParams *prm, size_t count,
+                                          const uint8_t *syn, const uint8_t *pos8, const uint32_t *pos32,
+                                          size_t pos_stride, const uint8_t *cnt, uint8_t *ok, uint8_t *corrected,
+                                          uint8_t *rec, uint8_t *meta, int num_cu, hipStream_t stream)
+{
+    if (count == 0)
+        return hipSuccess;
+    const dim3 grid(persistent_grid(count, COR_WG, num_cu));
+    if (pos32)
+        hipLaunchKernelGGL((rs_correct_k<uint32_t, true, true>), grid, dim3(COR_WG), 0, stream, tab, *prm, nullptr,
+                           0, nullptr, 0, count, syn, nullptr, 0, pos32, pos_stride, cnt, ok, corrected, nullptr,
+                           nullptr, rec, meta);
+    else
+        hipLaunchKernelGGL((rs_correct_k<uint8_t, true, true>), grid, dim3(COR_WG), 0, stream, tab, *prm, nullptr, 0,
+                           nullptr, 0, count, syn, nullptr, 0, pos8, pos_stride, cnt, ok, corrected, nullptr, nullptr,
+                           rec, meta);
+    return hipGetLastError();
+}
+
+/* the same over the codewords list[0 .. *list_n) that rs_era_k hands on */
+extern "C" hipError_t rsk_correct_era_list(const RsDevTables *tab, const RsCorrParams *prm, size_t count,
+                                           const uint8_t *syn, const uint8_t *pos8, size_t pos_stride,
+                                           const uint8_t *cnt, uint8_t *ok, uint8_t *corrected, uint8_t *rec,
+                                           uint8_t *meta, const uint32_t *list, const uint32_t *list_n, int num_cu,
+                                           hipStream_t stream)
+{
+    if (count == 0)
+        return hipSuccess;
+    /* full persistent grid: blocks past the list's length leave at once */
+    const dim3 grid(persistent_grid(count, COR_WG, num_cu));
+    hipLaunchKernelGGL((rs_correct_k<uint8_t, true, true>), grid, dim3(COR_WG), 0, stream, tab, *prm, nullptr, 0,
+                       nullptr, 0, count, syn, nullptr, 0, pos8, pos_stride, cnt, ok, corrected, list, list_n, rec,
+                       meta);
     return hipGetLastError();
 }

@@ -183,6 +183,32 @@ hipError_t rsk_forney(const RsDevTables *tab, const RsCorrParams *prm, const RsS
 hipError_t rsk_apply(const RsCorrParams *prm, const RsSplitWs *ws, uint8_t *data, size_t dstride, uint8_t *parity,
                      size_t pstride, size_t count, hipStream_t stream);
 
+/*
+ * Split erasure-mode decode, after rsk_syndrome into ws.syn:
+ *   rsk_correct_era_rec  the general kernel's erasure decode with the
+ *                        corrections written as 64-byte records (32 slot
+ *                        positions clamped to 255, 32 magnitudes) into rec,
+ *                        meta[cw] = RS_ST_FAST where a record was written
+ *   rsk_apply_era        the records into the codewords (rs_apply_k<32>)
+ * rec: the 64 * cap bytes from ws.lam (lam, om and roots back to back).
+ */
+hipError_t rsk_correct_era_rec(const RsDevTables *tab, const RsCorrParams *prm, size_t count, const uint8_t *syn,
+                               const uint8_t *pos8, const uint32_t *pos32, size_t pos_stride, const uint8_t *cnt,
+                               uint8_t *ok, uint8_t *corrected, uint8_t *rec, uint8_t *meta, int num_cu,
+                               hipStream_t stream);
+/* the 32-sorted-erasure kernel (rs_fast.hip: rs_era_k, prim 1, 16-byte
+ * aligned u8 slots): records for its codewords, clean ones finished, the rest
+ * onto ws.list (zeroed by rsk_syndrome_reset) for rsk_correct_era_list */
+hipError_t rsk_era(const RsDevTables *tab, const RsCorrParams *prm, const RsSplitWs *ws, const uint8_t *pos8,
+                   size_t pos_stride, const uint8_t *cnt, size_t count, uint8_t *ok, uint8_t *corrected, int num_cu,
+                   hipStream_t stream);
+hipError_t rsk_correct_era_list(const RsDevTables *tab, const RsCorrParams *prm, size_t count, const uint8_t *syn,
+                                const uint8_t *pos8, size_t pos_stride, const uint8_t *cnt, uint8_t *ok,
+                                uint8_t *corrected, uint8_t *rec, uint8_t *meta, const uint32_t *list,
+                                const uint32_t *list_n, int num_cu, hipStream_t stream);
+hipError_t rsk_apply_era(const RsCorrParams *prm, const uint8_t *meta, const uint8_t *rec, uint8_t *data,
+                         size_t dstride, uint8_t *parity, size_t pstride, size_t count, hipStream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

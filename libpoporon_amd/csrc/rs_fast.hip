@@ -783,6 +783,235 @@ __global__ __launch_bounds__(FWG, FORNEY_WAVES) void rs_forney_k(const RsDevTabl
 }
 
 /* ------------------------------------------------------------------------ */
+/* rs_era_k: erasure decode at num_roots known positions (configs[3])       */
+/* ------------------------------------------------------------------------ */
+
+/*
+ * Codewords with 32 erasures (= num_roots) in strictly ascending slots inside
+ * the codeword, prim = 1.  Berlekamp-Massey does not run (src/decode.c:53-55:
+ * r starts at the erasure count), so Lambda is the erasure locator
+ * prod(1 + X_l x) of :31-47, X_l = alpha^(254 - L_l), L_l = slot + pad, of
+ * degree 32 (every X_l nonzero).  Its roots are the Chien points (:117-141)
+ * i_l = L_l + 1, found in ascending order = slot order, so magnitude l goes
+ * to slot l (:211-214), and the count equals the degree.  Forney (:147-191)
+ * runs at those points; the re-syndrome check (:193-209) passes by
+ * construction (32 equations, 32 unknowns, distinct X_l).  Lambda_32 plays
+ * no part (Omega stops at x^31, Lambda' at x^30).  Everything else -- other
+ * counts, unsorted or repeated slots, slots past the codeword -- goes to the
+ * list (rs_correct_k in record mode).  Output: the 64-byte record of
+ * rs_apply_k<32> (slots, magnitudes).
+ *
+ * Registers (64 at 8 waves/SIMD): the locator in 31 address-form logs, then
+ * packed two per register for Omega (16 + 16 syndrome logs + 16 Omega) and
+ * Forney (Omega, odd Lambda: 24); slots are re-read where needed.
+ */
+#ifndef ERA_WAVES
+#define ERA_WAVES 4 /* 117 VGPRs, no spill: 0.388 ms; 6: 0.397, 8 (328 B spill): 0.407 */
+#endif
+#define ERA_R 4 /* Forney roots per step */
+
+__global__ __launch_bounds__(FWG, ERA_WAVES) void rs_era_k(const RsDevTables *__restrict__ T, RsCorrParams P,
+                                                         const uint8_t *__restrict__ syn,
+                                                         const uint8_t *__restrict__ pos8, size_t pos_stride,
+                                                         const uint8_t *__restrict__ cntp, size_t count,
+                                                         uint8_t *__restrict__ rec, uint8_t *__restrict__ meta,
+                                                         uint32_t *__restrict__ list, uint32_t *__restrict__ nlist,
+                                                         uint8_t *__restrict__ ok, uint8_t *__restrict__ corrected)
+{
+    __shared__ uint32_t lgf[512 * 32];
+    fill_gfa(lgf, T);
+    __syncthreads();
+    const GfA gf{lds_addr(lgf) + 4u * (threadIdx.x & 31u) + 1u};
+    const uint32_t pofs = gf.pofs;
+    const uint32_t AZ = gf.az();
+    constexpr uint32_t M255 = 255u * 128u;
+    /* x mod 255 on scaled logs / address forms: x < 2 * 255 * 128 + 128 */
+    auto red7 = [](uint32_t x) __attribute__((always_inline)) { return min(x, x - M255); };
+    const uint32_t lim = P.size + RS_NR, pad = (uint32_t)P.pad;
+
+    for (size_t base = (size_t)blockIdx.x * FWG; base < count; base += (size_t)gridDim.x * FWG) {
+        const size_t cw = base + threadIdx.x;
+        const bool valid = cw < count;
+        uint4 sa = make_uint4(0, 0, 0, 0), sb = sa, pa = sa, pb = sa;
+        uint32_t ne = 0;
+        const uint8_t *slots = pos8 + (valid ? cw : 0) * pos_stride;
+        if (valid) {
+            sa = reinterpret_cast<const uint4 *>(syn)[2 * cw];
+            sb = reinterpret_cast<const uint4 *>(syn)[2 * cw + 1];
+            pa = reinterpret_cast<const uint4 *>(slots)[0];
+            pb = reinterpret_cast<const uint4 *>(slots)[1];
+            ne = cntp[cw];
+        }
+        const bool any = (sa.x | sa.y | sa.z | sa.w | sb.x | sb.y | sb.z | sb.w) != 0u;
+        uint32_t pk[RS_NR / 4] = {pa.x, pa.y, pa.z, pa.w, pb.x, pb.y, pb.z, pb.w};
+        bool asc = true;
+        uint32_t prev = pk[0] & 0xffu;
+#pragma unroll
+        for (int n = 1; n < RS_NR; ++n) {
+            const uint32_t p = (pk[n >> 2] >> (8 * (n & 3))) & 0xffu;
+            asc = asc && p > prev;
+            prev = p;
+        }
+        const bool fast = valid && any && ne == RS_NR && asc && prev < lim;
+        if (valid && !fast) {
+            if (!any) {
+                ok[cw] = 1;
+                if (corrected)
+                    corrected[cw] = 0;
+                meta[cw] = (uint8_t)(RS_ST_DONE << 5);
+            } else {
+                meta[cw] = (uint8_t)(RS_ST_LIST << 5);
+                list[atomicAdd(nlist, 1u)] = (uint32_t)cw;
+            }
+        }
+        if (__ballot(fast) == 0ull) /* uniform */
+            continue;
+        uint32_t *recw = reinterpret_cast<uint32_t *>(rec + (valid ? cw : 0) * 64u);
+        if (fast) { /* the record's slots now: pa / pb need no registers past the locator */
+            reinterpret_cast<uint4 *>(recw)[0] = pa;
+            reinterpret_cast<uint4 *>(recw)[1] = pb;
+        }
+        if (!fast) { /* lanes along for the ride: any in-range slots */
+#pragma unroll
+            for (int k = 0; k < RS_NR / 4; ++k)
+                pk[k] = 0;
+        }
+
+        /* ---- erasure locator, src/decode.c:31-47: Lambda_j += X_l Lambda_(j-1),
+         * j = l+1 down to 1; the new top term X_l Lambda_l (Lambda_l != 0) is
+         * one add of logs ---- */
+        uint32_t al[RS_NR]; /* address-form logs of Lambda_0..31 */
+        al[0] = pofs;
+#pragma unroll
+        for (int j = 1; j < RS_NR; ++j)
+            al[j] = AZ;
+        static_for<0, RS_NR, 1>([&](auto lc) __attribute__((always_inline)) {
+            constexpr int l = decltype(lc)::value;
+            const uint32_t p = (pk[l >> 2] >> (8 * (l & 3))) & 0xffu;
+            const uint32_t xs = 128u * (254u - (p + pad)); /* scaled log X_l */
+            static_for<0, (l + 1 < RS_NR ? l + 1 : RS_NR - 1), 1>([&](auto kc) __attribute__((always_inline)) {
+                constexpr int j = (l + 1 < RS_NR ? l + 1 : RS_NR - 1) - decltype(kc)::value;
+                if constexpr (j == l + 1)
+                    al[j] = red7(al[j - 1] + xs);
+                else
+                    al[j] = gf.loga(gf.expa(al[j]) ^ gf.expa(al[j - 1] + xs));
+                if constexpr ((j & 7) == 0)
+                    __builtin_amdgcn_sched_barrier(0); /* eight terms at a time: registers */
+            });
+            __builtin_amdgcn_sched_barrier(0); /* one factor at a time: registers */
+        });
+        uint32_t alp[RS_NR / 2];
+#pragma unroll
+        for (int k = 0; k < RS_NR / 2; ++k)
+            alp[k] = al[2 * k] | (al[2 * k + 1] << 16);
+
+        /* ---- Omega = S Lambda mod x^32, src/decode.c:147-158 ---- */
+        uint32_t sl[RS_NR / 2]; /* plain scaled logs of S_0..31, two per register */
+        {
+            /* the syndromes again (L2): keeping them through the locator costs registers */
+            const uint8_t *sp = syn + (valid ? cw : 0) * RS_NR;
+            asm volatile("" : "+v"(sp));
+            sa = reinterpret_cast<const uint4 *>(sp)[0];
+            sb = reinterpret_cast<const uint4 *>(sp)[1];
+            const uint32_t sw[8] = {sa.x, sa.y, sa.z, sa.w, sb.x, sb.y, sb.z, sb.w};
+#pragma unroll
+            for (int k = 0; k < RS_NR; k += 2)
+                sl[k >> 1] = gf.logs((sw[k >> 2] >> (8 * (k & 3))) & 0xffu) |
+                             (gf.logs((sw[k >> 2] >> (8 * ((k + 1) & 3))) & 0xffu) << 16);
+        }
+        uint32_t ob[RS_NR / 4]; /* byte logs of Omega_0..31 (255 = zero), four per register */
+        static_for<0, RS_NR, 1>([&](auto mc) __attribute__((always_inline)) {
+            constexpr int m = decltype(mc)::value;
+            uint32_t acc = 0;
+            static_for<0, m + 1, 8>([&](auto gc) __attribute__((always_inline)) {
+                constexpr int g = decltype(gc)::value; /* eight lookups at a time: registers */
+#pragma unroll
+                for (int t = g; t <= m && t < g + 8; ++t)
+                    acc ^= gf.expa(half(alp, t) + half(sl, m - t));
+                asm volatile("" : "+v"(acc)); /* the sum now: no deferred xor tree */
+                __builtin_amdgcn_sched_barrier(0);
+            });
+            const uint32_t o = gf.plog(gf.loga(acc));
+            if constexpr ((m & 3) == 0)
+                ob[m >> 2] = o;
+            else
+                ob[m >> 2] |= o << (8 * (m & 3));
+            __builtin_amdgcn_sched_barrier(0); /* one coefficient's lookups at a time: registers */
+        });
+        uint32_t op[RS_NR / 2]; /* Omega_0..31 address-form, two per register */
+#pragma unroll
+        for (int k = 0; k < RS_NR / 2; ++k)
+            op[k] = gf.afrom((ob[k >> 1] >> (16 * (k & 1))) & 0xffu) |
+                    (gf.afrom((ob[k >> 1] >> (16 * (k & 1) + 8)) & 0xffu) << 16);
+        uint32_t alo[RS_NR / 4]; /* Lambda_1, 3, .., 31 */
+#pragma unroll
+        for (int k = 0; k < RS_NR / 4; ++k)
+            alo[k] = (alp[2 * k] >> 16) | (alp[2 * k + 1] & 0xffff0000u);
+
+        /* ---- Forney at the known roots, src/decode.c:159-191: num = sum_m
+         * Omega_m alpha^(i m), den = sum_h Lambda_(2h+1) alpha^(2h i),
+         * magnitude alpha^(log num + log alpha^(i (fcr-1)) + 255 - log den);
+         * a zero numerator corrects nothing and is not counted ---- */
+        uint32_t ncor = 0;
+        const uint32_t *slw = reinterpret_cast<const uint32_t *>(slots);
+#pragma unroll 1
+        for (uint32_t q = 0; q < RS_NR / ERA_R; ++q) {
+            const uint32_t w = fast ? slw[q] : 0u;
+            /* opaque per step: the halves are unpacked at their use, not
+             * hoisted out of the loop (48 registers) */
+#pragma unroll
+            for (int k = 0; k < RS_NR / 2; ++k)
+                asm volatile("" : "+v"(op[k]));
+#pragma unroll
+            for (int k = 0; k < RS_NR / 4; ++k)
+                asm volatile("" : "+v"(alo[k]));
+            uint32_t ii[ERA_R], si[ERA_R], s[ERA_R], num[ERA_R], den[ERA_R];
+#pragma unroll
+            for (int t = 0; t < ERA_R; ++t) {
+                ii[t] = ((w >> (8 * t)) & 0xffu) + pad + 1u; /* the Chien point, 1..255 */
+                si[t] = 128u * (ii[t] == 255u ? 0u : ii[t]);
+                s[t] = 0;
+                num[t] = 0;
+                den[t] = 0;
+            }
+#pragma unroll
+            for (int m = 0; m < RS_NR; ++m) {
+#pragma unroll
+                for (int t = 0; t < ERA_R; ++t) {
+                    num[t] ^= gf.expa(half(op, m) + s[t]);
+                    if ((m & 1) == 0)
+                        den[t] ^= gf.expa(half(alo, m >> 1) + s[t]);
+                    s[t] = red7(s[t] + si[t]);
+                }
+                if (m & 1) {
+#pragma unroll
+                    for (int t = 0; t < ERA_R; ++t)
+                        asm volatile("" : "+v"(num[t]), "+v"(den[t]));
+                    __builtin_amdgcn_sched_barrier(0); /* two powers at a time: registers */
+                }
+            }
+            uint32_t cur = 0;
+#pragma unroll
+            for (int t = 0; t < ERA_R; ++t) {
+                const uint32_t ln2 = mod255((uint32_t)((int32_t)ii[t] * ((int32_t)P.fcr - 1) + (int32_t)RS_NN));
+                const uint32_t lnum = gf.plog(gf.loga(num[t])), lden = gf.plog(gf.loga(den[t]));
+                const bool z = num[t] != 0u;
+                ncor += z ? 1u : 0u;
+                cur |= (z ? gf.exp((lnum + ln2 + RS_NN - lden) % 255u) : 0u) << (8 * t);
+            }
+            if (fast)
+                recw[8 + q] = cur;
+        }
+        if (fast) {
+            meta[cw] = (uint8_t)(RS_ST_FAST << 5);
+            ok[cw] = 1;
+            if (corrected)
+                corrected[cw] = (uint8_t)ncor;
+        }
+    }
+}
+
+/* ------------------------------------------------------------------------ */
 /* rs_apply_k: the corrections, src/decode.c:215-226                         */
 /* ------------------------------------------------------------------------ */
 
@@ -800,10 +1029,12 @@ __global__ __launch_bounds__(FWG, FORNEY_WAVES) void rs_forney_k(const RsDevTabl
 #define AWG 256                 /* 4 waves, 16,320 B of LDS each */
 #define ABLK (64u * 255u / 16u) /* 16-byte chunks per wave block: 1020 */
 
+template <int NC> /* corrections per record: 16 (error mode) or 32 (erasure mode) */
 __global__ __launch_bounds__(AWG) void rs_apply_k(const uint8_t *__restrict__ meta, const uint8_t *__restrict__ rec,
                                                   uint8_t *data, size_t dstride, uint8_t *parity, size_t pstride,
                                                   uint32_t size, size_t count, uint32_t wire)
 {
+    constexpr int NW = NC / 4; /* record dwords of positions (then as many of magnitudes) */
     __shared__ uint4 img[AWG / 64][ABLK];
     const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63u;
 #if APPLY_REV /* last blocks first: the codewords the syndrome pass read last may still sit in the MALL */
@@ -816,15 +1047,23 @@ __global__ __launch_bounds__(AWG) void rs_apply_k(const uint8_t *__restrict__ me
     const size_t cw = base + lane;
     const bool valid = cw < count;
     const bool fast = valid && (meta[cw] >> 5) == RS_ST_FAST;
-    uint4 pos4 = make_uint4(0, 0, 0, 0), mag4 = pos4;
+    uint32_t pw[NW], mw[NW];
+#pragma unroll
+    for (int k = 0; k < NW; ++k)
+        pw[k] = mw[k] = 0;
     if (fast) {
-        const uint4 *r = reinterpret_cast<const uint4 *>(rec + cw * 32u);
-        pos4 = r[0];
-        mag4 = r[1];
+        const uint4 *r = reinterpret_cast<const uint4 *>(rec + cw * (2u * NC));
+#pragma unroll
+        for (int k = 0; k < NW / 4; ++k) {
+            const uint4 a = r[k], b = r[NW / 4 + k];
+            pw[4 * k] = a.x, pw[4 * k + 1] = a.y, pw[4 * k + 2] = a.z, pw[4 * k + 3] = a.w;
+            mw[4 * k] = b.x, mw[4 * k + 1] = b.y, mw[4 * k + 2] = b.z, mw[4 * k + 3] = b.w;
+        }
     }
     if (__ballot(fast) == 0ull)
         return;
-    const uint32_t pw[4] = {pos4.x, pos4.y, pos4.z, pos4.w}, mw[4] = {mag4.x, mag4.y, mag4.z, mag4.w};
+    /* positions past the codeword (erasure slots, clamped to 255) are never written */
+    const uint32_t lim = size + RS_NR;
     if (wire && base + 64u <= count) { /* uniform */
         const uint4 *src = reinterpret_cast<const uint4 *>(data + base * 255u);
         uint4 *dst = reinterpret_cast<uint4 *>(data + base * 255u);
@@ -840,10 +1079,11 @@ __global__ __launch_bounds__(AWG) void rs_apply_k(const uint8_t *__restrict__ me
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         uint32_t *imw = reinterpret_cast<uint32_t *>(im);
 #pragma unroll
-        for (int n = 0; n < 16; ++n) {
+        for (int n = 0; n < NC; ++n) {
             const uint32_t mg = (mw[n >> 2] >> (8 * (n & 3))) & 0xffu;
-            if (mg) {
-                const uint32_t b = lane * 255u + ((pw[n >> 2] >> (8 * (n & 3))) & 0xffu);
+            const uint32_t p = (pw[n >> 2] >> (8 * (n & 3))) & 0xffu;
+            if (mg && p < lim) {
+                const uint32_t b = lane * 255u + p;
                 atomicXor(imw + (b >> 2), mg << (8u * (b & 3u)));
             }
         }
@@ -859,12 +1099,12 @@ __global__ __launch_bounds__(AWG) void rs_apply_k(const uint8_t *__restrict__ me
     } else if (fast) {
         uint8_t *cdata = data + cw * dstride, *cpar = parity + cw * pstride;
 #pragma unroll
-        for (int n = 0; n < 16; ++n) {
+        for (int n = 0; n < NC; ++n) {
             const uint32_t mg = (mw[n >> 2] >> (8 * (n & 3))) & 0xffu;
-            if (mg) {
-                const uint32_t p = (pw[n >> 2] >> (8 * (n & 3))) & 0xffu;
+            const uint32_t p = (pw[n >> 2] >> (8 * (n & 3))) & 0xffu;
+            if (mg && p < lim) {
                 uint8_t *d = p < size ? cdata + p : cpar + (p - size);
-                *d = (uint8_t)(*d ^ mg);
+                *d = (uint8_t)(*d ^ mg); /* in slot order: repeated slots accumulate */
             }
         }
     }
@@ -917,15 +1157,39 @@ extern "C" hipError_t rsk_forney(const RsDevTables *tab, const RsCorrParams *prm
     return hipGetLastError();
 }
 
-extern "C" hipError_t rsk_apply(const RsCorrParams *prm, const RsSplitWs *ws, uint8_t *data, size_t dstride,
-                                uint8_t *parity, size_t pstride, size_t count, hipStream_t stream)
+template <int NC>
+static hipError_t apply_launch(const RsCorrParams *prm, const uint8_t *meta, const uint8_t *rec, uint8_t *data,
+                               size_t dstride, uint8_t *parity, size_t pstride, size_t count, hipStream_t stream)
 {
     if (count == 0)
         return hipSuccess;
     const uint32_t wire = prm->size == 223u && dstride == 255u && pstride == 255u && parity == data + 223 &&
                           (reinterpret_cast<uintptr_t>(data) & 15u) == 0u;
     const size_t waves = (count + 63) / 64;
-    hipLaunchKernelGGL(rs_apply_k, dim3((uint32_t)((waves + AWG / 64 - 1) / (AWG / 64))), dim3(AWG), 0, stream,
-                       ws->meta, ws->roots, data, dstride, parity, pstride, prm->size, count, wire);
+    hipLaunchKernelGGL(rs_apply_k<NC>, dim3((uint32_t)((waves + AWG / 64 - 1) / (AWG / 64))), dim3(AWG), 0, stream,
+                       meta, rec, data, dstride, parity, pstride, prm->size, count, wire);
+    return hipGetLastError();
+}
+
+extern "C" hipError_t rsk_apply(const RsCorrParams *prm, const RsSplitWs *ws, uint8_t *data, size_t dstride,
+                                uint8_t *parity, size_t pstride, size_t count, hipStream_t stream)
+{
+    return apply_launch<16>(prm, ws->meta, ws->roots, data, dstride, parity, pstride, count, stream);
+}
+
+extern "C" hipError_t rsk_apply_era(const RsCorrParams *prm, const uint8_t *meta, const uint8_t *rec, uint8_t *data,
+                                    size_t dstride, uint8_t *parity, size_t pstride, size_t count, hipStream_t stream)
+{
+    return apply_launch<32>(prm, meta, rec, data, dstride, parity, pstride, count, stream);
+}
+
+extern "C" hipError_t rsk_era(const RsDevTables *tab, const RsCorrParams *prm, const RsSplitWs *ws, const uint8_t *pos8,
+                              size_t pos_stride, const uint8_t *cnt, size_t count, uint8_t *ok, uint8_t *corrected,
+                              int num_cu, hipStream_t stream)
+{
+    if (count == 0)
+        return hipSuccess;
+    hipLaunchKernelGGL(rs_era_k, dim3(fast_grid(count, num_cu)), dim3(FWG), 0, stream, tab, *prm, ws->syn, pos8,
+                       pos_stride, cnt, count, ws->lam, ws->meta, ws->list, ws->nlist, ok, corrected);
     return hipGetLastError();
 }

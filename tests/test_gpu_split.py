@@ -177,3 +177,71 @@ def torch_cuda_split():
     import torch
     assert torch.cuda.is_available()
     return torch
+
+
+def _erasure_batch(rng, h, n, size, dup):
+    data = rng.integers(0, 256, (n, size), dtype=np.uint8)
+    cw = np.concatenate([data, h.encode_batch(data)], 1)
+    L = size + NR
+    slots = np.zeros((n, NR), np.uint8)
+    cnt = rng.integers(0, NR + 1, n).astype(np.uint8)
+    cnt[: n // 3] = NR  # the configs[3] case, many of them
+    for c in range(n):
+        e = int(cnt[c])
+        slots[c] = rng.permutation(255)[:NR] if c % 5 == 0 else rng.permutation(L)[:NR]  # some past the row
+        if c % 2:
+            slots[c, :e] = np.sort(slots[c, :e])
+        if dup:
+            slots[c, e:] = rng.integers(0, 4, NR - e)  # stale slots repeating positions (quirk Q2)
+        inrow = slots[c, :e][slots[c, :e] < L]
+        cw[c, inrow] ^= rng.integers(1, 256, inrow.size, dtype=np.uint8)
+        x = int(rng.integers(0, max(1, (NR - e) // 2 + 2)))
+        cw[c, rng.permutation(L)[:x]] ^= rng.integers(1, 256, x, dtype=np.uint8)
+    return cw, slots, cnt
+
+
+@pytest.mark.parametrize("path", PATHS)
+@pytest.mark.parametrize("size,dup", [(223, False), (223, True), (200, False)])
+def test_split_erasures_vs_oracle(monkeypatch, oracle_default, path, size, dup):
+    """Erasure batches through the record + block-apply path (split) and the
+    single kernel: 0..32 slots, sorted and unsorted, slots past the codeword,
+    repeated stale slots, extra errors -- bit for bit against the oracle."""
+    h = _handle(monkeypatch, path)
+    rng = np.random.default_rng(500 + size + dup)
+    cw, slots, cnt = _erasure_batch(rng, h, 12000, size, dup)
+    got = h.decode_batch(cw[:, :size], cw[:, size:], slots, cnt)
+    want = oracle_default.decode_batch(cw[:, :size], cw[:, size:], slots.astype(np.uint32), cnt.astype(np.uint32))
+    assert want[0].sum() > 1000
+    _same(got, want)
+
+
+def test_split_erasure_kernels_timed(monkeypatch, torch_cuda_split):
+    """A 2^16 batch with 32 sorted erasures each: remainder, rs_era_k, the
+    (empty) list, block apply -- codewords restored, 32 corrections each."""
+    torch = torch_cuda_split
+    h = _handle(monkeypatch, "split")
+    n = 1 << 16
+    g = torch.Generator(device="cuda")
+    g.manual_seed(9)
+    cw = torch.randint(0, 256, (n, 255), dtype=torch.uint8, device="cuda", generator=g)
+    s = torch.cuda.current_stream().cuda_stream
+    base = cw.data_ptr()
+    h.encode_batch_device(base, 255, base + 223, 255, 223, n, s)
+    clean = cw.clone()
+    pos = torch.rand((n, 223), device="cuda", generator=g).topk(NR, dim=1).indices.sort(dim=1).values
+    mag = torch.randint(1, 256, (n, NR), dtype=torch.uint8, device="cuda", generator=g)
+    cw.scatter_(1, pos, cw.gather(1, pos) ^ mag)
+    slots = pos.to(torch.uint8).contiguous()
+    cnt = torch.full((n,), NR, dtype=torch.uint8, device="cuda")
+    ok = torch.zeros(n, dtype=torch.uint8, device="cuda")
+    cor = torch.zeros(n, dtype=torch.uint8, device="cuda")
+    h.timing(True)
+    h.decode_batch_device(base, 255, base + 223, 255, 223, n, ok.data_ptr(), cor.data_ptr(),
+                          d_positions=slots.data_ptr(), positions_stride=NR, d_counts=cnt.data_ptr(), stream=s)
+    torch.cuda.synchronize()
+    t = {k: h.timing_read(k) for k in P.KERNEL_NAMES}
+    h.timing(False)
+    assert torch.equal(cw, clean) and int(ok.sum()) == n and bool((cor == NR).all())
+    for k in (P.KERNEL_REMAINDER, P.KERNEL_ERASURE, P.KERNEL_LIST, P.KERNEL_APPLY):
+        assert t[k][1] == 1, (k, t[k])
+    assert t[P.KERNEL_CORRECT][1] == 0

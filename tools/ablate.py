@@ -46,7 +46,8 @@ def main():
         times = []
         for rep in range(6):
             cw.copy_(clean)
-            cw.scatter_(1, pos, cw.gather(1, pos) ^ mag)
+            pl = pos.long()
+            cw.scatter_(1, pl, cw.gather(1, pl) ^ mag)
             torch.cuda.synchronize()
             rs.timing(True)
             rs.decode_batch_device(b, N, b + K, N, K, n, ok.data_ptr(), cor.data_ptr(), stream=s, **kw)
