@@ -806,9 +806,12 @@ __global__ __launch_bounds__(FWG, FORNEY_WAVES) void rs_forney_k(const RsDevTabl
  * Forney (Omega, odd Lambda: 24); slots are re-read where needed.
  */
 #ifndef ERA_WAVES
-#define ERA_WAVES 4 /* 117 VGPRs, no spill: 0.388 ms; 6: 0.397, 8 (328 B spill): 0.407 */
+#define ERA_WAVES 6 /* 80 VGPRs: 0.351 ms per 2^20 codewords; 4: 0.358, 8 (a few spills outside the loops): 0.365 */
 #endif
-#define ERA_R 4 /* Forney roots per step */
+#define ERA_R 4 /* Forney roots per step: one record dword */
+#ifndef ERA_OG
+#define ERA_OG 8 /* Omega lookups per group */
+#endif
 
 __global__ __launch_bounds__(FWG, ERA_WAVES) void rs_era_k(const RsDevTables *__restrict__ T, RsCorrParams P,
                                                          const uint8_t *__restrict__ syn,
@@ -922,11 +925,15 @@ __global__ __launch_bounds__(FWG, ERA_WAVES) void rs_era_k(const RsDevTables *__
         uint32_t ob[RS_NR / 4]; /* byte logs of Omega_0..31 (255 = zero), four per register */
         static_for<0, RS_NR, 1>([&](auto mc) __attribute__((always_inline)) {
             constexpr int m = decltype(mc)::value;
+            /* opaque per coefficient: halves unpacked at their use, not all at once */
+#pragma unroll
+            for (int k = 0; k < RS_NR / 2; ++k)
+                asm volatile("" : "+v"(alp[k]), "+v"(sl[k]));
             uint32_t acc = 0;
-            static_for<0, m + 1, 8>([&](auto gc) __attribute__((always_inline)) {
+            static_for<0, m + 1, ERA_OG>([&](auto gc) __attribute__((always_inline)) {
                 constexpr int g = decltype(gc)::value; /* eight lookups at a time: registers */
 #pragma unroll
-                for (int t = g; t <= m && t < g + 8; ++t)
+                for (int t = g; t <= m && t < g + ERA_OG; ++t)
                     acc ^= gf.expa(half(alp, t) + half(sl, m - t));
                 asm volatile("" : "+v"(acc)); /* the sum now: no deferred xor tree */
                 __builtin_amdgcn_sched_barrier(0);
