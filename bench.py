@@ -409,12 +409,14 @@ def run_erasure(be, ranks, args, rank, world, w):
         estep(1 + k)
     ranks.barrier(be.sync)
     et = ranks.max(time.perf_counter() - t0)
-    kms = sum(ms / max(1, n) for ms, n in (be.rs.timing_read(k) for k in be.P.KERNEL_NAMES) if n)
+    ekt = {be.P.KERNEL_NAMES[k]: be.rs.timing_read(k) for k in be.P.KERNEL_NAMES}
+    kms = sum(ms / n for ms, n in ekt.values() if n)
     be.rs.timing(False)
     enbad = be.n_bad(w["st"], 32) + sum(be.n_diff(b, eclean) for b in (ebad[1:] if ecopies else [cw]))
     enbad = ranks.sum_int(enbad)
     return {"cw_per_s": round(B * world * es / et, 1),
             "kernel_cw_per_s_per_gpu": round(B / (kms * 1e-3), 1) if kms else None,
+            "kernels_avg_ms": {name: round(ms / n, 4) for name, (ms, n) in ekt.items() if n},
             "positions_bytes_per_cw": 32,
             "verified": enbad == 0,
             "channel": "outside the timed decodes (one corrupted copy per decode)" if ecopies
