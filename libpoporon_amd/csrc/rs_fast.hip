@@ -880,33 +880,59 @@ __global__ __launch_bounds__(FWG, ERA_WAVES) void rs_era_k(const RsDevTables *__
                 pk[k] = 0;
         }
 
-        /* ---- erasure locator, src/decode.c:31-47: Lambda_j += X_l Lambda_(j-1),
-         * j = l+1 down to 1; the new top term X_l Lambda_l (Lambda_l != 0) is
-         * one add of logs ---- */
-        uint32_t al[RS_NR]; /* address-form logs of Lambda_0..31 */
-        al[0] = pofs;
+        /* ---- erasure locator, src/decode.c:31-47, as the product of two
+         * halves A = prod_(l<16), B = prod_(l>=16) (the same field elements;
+         * 1,038 lookups instead of 1,395).  Each half incrementally:
+         * H_j += X_l H_(j-1), j = l+1 down to 1, the new top term X_l H_l
+         * (nonzero) one add of logs ---- */
+        constexpr int NH = RS_NR / 2;
+        auto half_locator = [&](uint32_t (&h)[NH + 1], auto l0c) __attribute__((always_inline)) {
+            constexpr int L0 = decltype(l0c)::value;
+            h[0] = pofs;
 #pragma unroll
-        for (int j = 1; j < RS_NR; ++j)
-            al[j] = AZ;
-        static_for<0, RS_NR, 1>([&](auto lc) __attribute__((always_inline)) {
-            constexpr int l = decltype(lc)::value;
-            const uint32_t p = (pk[l >> 2] >> (8 * (l & 3))) & 0xffu;
-            const uint32_t xs = 128u * (254u - (p + pad)); /* scaled log X_l */
-            static_for<0, (l + 1 < RS_NR ? l + 1 : RS_NR - 1), 1>([&](auto kc) __attribute__((always_inline)) {
-                constexpr int j = (l + 1 < RS_NR ? l + 1 : RS_NR - 1) - decltype(kc)::value;
-                if constexpr (j == l + 1)
-                    al[j] = red7(al[j - 1] + xs);
-                else
-                    al[j] = gf.loga(gf.expa(al[j]) ^ gf.expa(al[j - 1] + xs));
-                if constexpr ((j & 7) == 0)
-                    __builtin_amdgcn_sched_barrier(0); /* eight terms at a time: registers */
+            for (int j = 1; j <= NH; ++j)
+                h[j] = AZ;
+            static_for<0, NH, 1>([&](auto lc) __attribute__((always_inline)) {
+                constexpr int l = decltype(lc)::value, lg = L0 + l;
+                const uint32_t p = (pk[lg >> 2] >> (8 * (lg & 3))) & 0xffu;
+                const uint32_t xs = 128u * (254u - (p + pad)); /* scaled log X_l */
+                static_for<0, l + 1, 1>([&](auto kc) __attribute__((always_inline)) {
+                    constexpr int j = l + 1 - decltype(kc)::value;
+                    if constexpr (j == l + 1)
+                        h[j] = red7(h[j - 1] + xs);
+                    else
+                        h[j] = gf.loga(gf.expa(h[j]) ^ gf.expa(h[j - 1] + xs));
+                    if constexpr ((j & 7) == 0)
+                        __builtin_amdgcn_sched_barrier(0); /* eight terms at a time: registers */
+                });
+                __builtin_amdgcn_sched_barrier(0); /* one factor at a time: registers */
             });
-            __builtin_amdgcn_sched_barrier(0); /* one factor at a time: registers */
-        });
-        uint32_t alp[RS_NR / 2];
+        };
+        uint32_t ha[NH + 1], hb[NH + 1]; /* address-form logs of A_0..16, B_0..16 */
+        half_locator(ha, std::integral_constant<int, 0>{});
+        half_locator(hb, std::integral_constant<int, NH>{});
 #pragma unroll
-        for (int k = 0; k < RS_NR / 2; ++k)
-            alp[k] = al[2 * k] | (al[2 * k + 1] << 16);
+        for (int j = 0; j <= NH; ++j)
+            hb[j] -= pofs; /* plain scaled logs (zero: SZ) */
+        /* Lambda_k = sum_(i+j=k) A_i B_j, k < 32 (Lambda_32 plays no part) */
+        uint32_t alp[RS_NR / 2]; /* address-form logs of Lambda_0..31, two per register */
+        static_for<0, RS_NR, 1>([&](auto kc) __attribute__((always_inline)) {
+            constexpr int k = decltype(kc)::value;
+            uint32_t o = pofs;
+            if constexpr (k > 0) {
+                uint32_t acc = 0;
+#pragma unroll
+                for (int i = (k > NH ? k - NH : 0); i <= (k < NH ? k : NH); ++i)
+                    acc ^= gf.expa(ha[i] + hb[k - i]);
+                asm volatile("" : "+v"(acc));
+                o = gf.loga(acc);
+            }
+            if constexpr (k & 1)
+                alp[k >> 1] |= o << 16;
+            else
+                alp[k >> 1] = o;
+            __builtin_amdgcn_sched_barrier(0); /* one coefficient at a time: registers */
+        });
 
         /* ---- Omega = S Lambda mod x^32, src/decode.c:147-158 ---- */
         uint32_t sl[RS_NR / 2]; /* plain scaled logs of S_0..31, two per register */

@@ -245,3 +245,19 @@ def test_split_erasure_kernels_timed(monkeypatch, torch_cuda_split):
     for k in (P.KERNEL_REMAINDER, P.KERNEL_ERASURE, P.KERNEL_LIST, P.KERNEL_APPLY):
         assert t[k][1] == 1, (k, t[k])
     assert t[P.KERNEL_CORRECT][1] == 0
+
+
+@pytest.mark.parametrize("params", [(8, 0x11D, 0, 1, 32), (8, 0x187, 5, 1, 32), (8, 0x11D, 1, 2, 32),
+                                    (8, 0x11D, 5, 7, 32)])
+def test_split_erasures_other_parameters_vs_oracle(monkeypatch, params):
+    """Erasure batches under other fcr / prim / field polynomials: rs_era_k
+    (prim 1, any fcr) and the record-mode general kernel (prim != 1)."""
+    from oracle import Oracle
+    o = Oracle(*params)
+    h = _handle(monkeypatch, "split", params)
+    rng = np.random.default_rng(sum(params) + 7)
+    cw, slots, cnt = _erasure_batch(rng, h, 9000, 223, False)
+    got = h.decode_batch(cw[:, :223], cw[:, 223:], slots, cnt)
+    want = o.decode_batch(cw[:, :223], cw[:, 223:], slots.astype(np.uint32), cnt.astype(np.uint32))
+    assert want[0].sum() > 1000
+    _same(got, want)
