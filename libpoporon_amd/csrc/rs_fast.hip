@@ -737,9 +737,8 @@ __global__ __launch_bounds__(FWG, FORNEY_WAVES) void rs_forney_k(const RsDevTabl
                             nm[t] ^= gf.expa(OMLOG(m) + ie[t]);
                             den[t] ^= gf.expa(LODD(m >> 1) + ie[t]);
                             nm[t] ^= gf.expa(OMLOG(m + 1) + io[t]);
-                            const uint32_t te = ie[t] + i2[t], to = io[t] + i2[t];
-                            ie[t] = min(te, te - 255u * 128u);
-                            io[t] = min(to, to - 255u * 128u);
+                            ie[t] = addmod7(ie[t], i2[t]);
+                            io[t] = addmod7(io[t], i2[t]);
                         }
                     }
                 }
@@ -1014,7 +1013,7 @@ __global__ __launch_bounds__(FWG, ERA_WAVES) void rs_era_k(const RsDevTables *__
                     num[t] ^= gf.expa(half(op, m) + s[t]);
                     if ((m & 1) == 0)
                         den[t] ^= gf.expa(half(alo, m >> 1) + s[t]);
-                    s[t] = red7(s[t] + si[t]);
+                    s[t] = addmod7(s[t], si[t]);
                 }
                 if (m & 1) {
 #pragma unroll

@@ -47,6 +47,26 @@ __device__ __forceinline__ uint32_t half(const uint32_t *a, int i)
     return (i & 1) ? (a[i >> 1] >> 16) : (a[i >> 1] & 0xffffu);
 }
 
+#ifndef U16RED
+#define U16RED 1
+#endif
+/* (x + y) mod 255 * 128 for scaled logs x, y < 255 * 128: three full-rate
+ * 16-bit ops instead of add, add, half-rate v_min_u32 (gfx950's VOP2 16-bit
+ * ops zero bits 31:16 of the result: tools/probes/u16_hi.hip) */
+__device__ __forceinline__ uint32_t addmod7(uint32_t x, uint32_t y)
+{
+#if U16RED
+    uint32_t t, u, r;
+    asm("v_add_u16 %0, %1, %2" : "=v"(t) : "v"(x), "v"(y));
+    asm("v_subrev_u16 %0, 0x7f80, %1" : "=v"(u) : "v"(t)); /* t - 255 * 128, wraps above t when t < 255 * 128 */
+    asm("v_min_u16 %0, %1, %2" : "=v"(r) : "v"(t), "v"(u));
+    return r;
+#else
+    const uint32_t t = x + y;
+    return min(t, t - 255u * 128u);
+#endif
+}
+
 /* a ^ b ^ c in one VALU op (gfx950 v_bitop3_b32, truth table 0x96) */
 __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c)
 {
