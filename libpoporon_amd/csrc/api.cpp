@@ -1090,8 +1090,11 @@ static bool launch_split(poporon_t *h, const RsCorrParams &prm, const RsSplitWs 
     GpuCtx &g = h->gpu;
     {
         KernelTimer t(g, POPORON_AMD_KERNEL_REMAINDER, s);
-        HIP_OK(rsk_syndrome_reset(g.tab, d_data, ds, d_par, ps, (uint32_t)size, count, ws.syn, ws.nlist, g.num_cu,
-                                  s));
+        if (count == 1)
+            HIP_OK(rsk_syndrome1(g.tab, prm.fcr, prm.prim, d_data, d_par, (uint32_t)size, ws.syn, ws.nlist, s));
+        else
+            HIP_OK(rsk_syndrome_reset(g.tab, d_data, ds, d_par, ps, (uint32_t)size, count, ws.syn, ws.nlist,
+                                      g.num_cu, s));
         t.done();
     }
     {
@@ -1219,7 +1222,10 @@ static bool launch_decode(poporon_t *h, uint8_t *d_data, size_t ds, uint8_t *d_p
     }
     if (!ext_syn) {
         KernelTimer t(h->gpu, POPORON_AMD_KERNEL_REMAINDER, s);
-        HIP_OK(rsk_syndrome(h->gpu.tab, d_data, ds, d_par, ps, (uint32_t)size, count, rem, h->gpu.num_cu, s));
+        if (count == 1) /* one codeword: the LFSR's 255 dependent steps are the latency */
+            HIP_OK(rsk_syndrome1(h->gpu.tab, prm.fcr, prm.prim, d_data, d_par, (uint32_t)size, rem, nullptr, s));
+        else
+            HIP_OK(rsk_syndrome(h->gpu.tab, d_data, ds, d_par, ps, (uint32_t)size, count, rem, h->gpu.num_cu, s));
         t.done();
     }
     KernelTimer t(h->gpu, POPORON_AMD_KERNEL_CORRECT, s);

@@ -135,6 +135,11 @@ hipError_t rsk_syndrome_reset(const RsDevTables *tab, const uint8_t *data, size_
                               size_t pstride, uint32_t size, size_t count, uint8_t *syn, uint32_t *reset, int num_cu,
                               hipStream_t stream);
 
+/* the same for one codeword (data, parity: its bytes), by direct evaluation
+ * on one workgroup: the single-call latency path; reset as above (may be NULL) */
+hipError_t rsk_syndrome1(const RsDevTables *tab, uint32_t fcr, uint32_t prim, const uint8_t *data,
+                         const uint8_t *parity, uint32_t size, uint8_t *syn, uint32_t *reset, hipStream_t stream);
+
 /* poly syndromes (32 B per codeword, rsk_syndrome) -> log form: out[c*stride + i]
  * = log S_i (255 = zero), flag[c] = any S_i nonzero; out / flag may be NULL */
 hipError_t rsk_syn_log(const RsDevTables *tab, const uint8_t *syn, size_t count, uint16_t *out, size_t stride,

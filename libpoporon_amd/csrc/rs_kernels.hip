@@ -544,6 +544,53 @@ extern "C" hipError_t rsk_syndrome_reset(const RsDevTables *tab, const uint8_t *
     return launch_lfsr<MODE_SYNDROME>(tab, data, dstride, parity, pstride, size, count, syn, num_cu, stream, reset);
 }
 
+/* One codeword's syndromes by direct evaluation (the single-call path, where
+ * the LFSR's 255 dependent steps on one lane are the latency): S_i =
+ * sum_j w_j beta_i^(L-1-j), w = data || parity, L = size + 32, beta_i =
+ * alpha^(prim (fcr + i)) -- the field elements of src/decode.c:375-415 and of
+ * the remainder kernel.  Thread t: syndrome t & 31 over bytes j = t >> 5
+ * (mod 8); the eight partial sums are XORed in LDS. */
+__global__ __launch_bounds__(256) void rs_syn1_k(const RsDevTables *__restrict__ T, uint32_t fcr, uint32_t prim,
+                                                 const uint8_t *__restrict__ data, const uint8_t *__restrict__ parity,
+                                                 uint32_t size, uint8_t *__restrict__ syn, uint32_t *__restrict__ reset)
+{
+    __shared__ uint8_t ex[512];
+    __shared__ uint8_t lg[256];
+    __shared__ uint32_t part[256];
+    const uint32_t t = threadIdx.x;
+    ex[t] = T->exp2[t];
+    ex[t + 256] = T->exp2[t + 256];
+    lg[t] = T->log[t];
+    if (reset && t == 0)
+        *reset = 0;
+    __syncthreads();
+    const uint32_t i = t & 31u, L = size + RS_NR;
+    const uint32_t b = (prim * (fcr + i)) % 255u;
+    uint32_t acc = 0;
+    for (uint32_t j = t >> 5; j < L; j += 8) {
+        const uint32_t w = j < size ? data[j] : parity[j - size];
+        if (w)
+            acc ^= ex[lg[w] + (b * (L - 1u - j)) % 255u];
+    }
+    part[t] = acc;
+    __syncthreads();
+    if (t < RS_NR) {
+        uint32_t v = 0;
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+            v ^= part[t + 32u * k];
+        syn[t] = (uint8_t)v;
+    }
+}
+
+extern "C" hipError_t rsk_syndrome1(const RsDevTables *tab, uint32_t fcr, uint32_t prim, const uint8_t *data,
+                                    const uint8_t *parity, uint32_t size, uint8_t *syn, uint32_t *reset,
+                                    hipStream_t stream)
+{
+    hipLaunchKernelGGL(rs_syn1_k, dim3(1), dim3(256), 0, stream, tab, fcr, prim, data, parity, size, syn, reset);
+    return hipGetLastError();
+}
+
 /* poly-form syndromes (rsk_syndrome's output) -> the reference's log form:
  * uint16 log S_i (255 = zero) and the "any nonzero" flag (src/decode.c:409-414) */
 __global__ __launch_bounds__(256) void rs_synlog_k(const RsDevTables *__restrict__ T, const uint8_t *__restrict__ syn,
