@@ -436,6 +436,22 @@ static void build_tables(poporon_t *h)
         memcpy(&t.lfsr[fb * 2], il, 16);
         memcpy(&t.lfsr[fb * 2 + 1], il + 4, 16);
     }
+    /* encq: the LFSR above run on the message 1, 0, 0, ... (rs_enc1_k) */
+    {
+        uint8_t q[RS_NR];
+        for (uint32_t m = 0; m < RS_NR; m++) /* one step with feedback 1 */
+            q[m] = (uint8_t)gf->log2exp[gf_mod(gf, g[RS_NR - 1 - m])];
+        for (uint32_t d = 0; d < 223; d++) {
+            for (uint32_t m = 0; m < RS_NR; m++)
+                t.encq[d * RS_NR + m] = (uint8_t)gf->exp2log[q[m]];
+            const uint32_t fb = q[0]; /* next step, input byte 0 */
+            for (uint32_t m = 0; m < RS_NR; m++) {
+                const uint8_t sh = m + 1 < RS_NR ? q[m + 1] : 0;
+                q[m] = sh ^ (fb == 0 ? 0
+                                     : (uint8_t)gf->log2exp[gf_mod(gf, (uint16_t)(gf->exp2log[fb] + g[RS_NR - 1 - m]))]);
+            }
+        }
+    }
     for (uint32_t x = 0; x < 512; x++)
         t.exp2[x] = (uint8_t)gf->log2exp[x % 255];
     t.exp2[511] = 0; /* ZLOG sentinel of the correction kernel (no sum of two logs reaches 511) */
@@ -1067,6 +1083,8 @@ static bool launch_encode(poporon_t *h, const uint8_t *d_data, size_t ds, uint8_
     KernelTimer t(h->gpu, POPORON_AMD_KERNEL_ENCODE, s);
     if (h->fec_type == PPLN_FEC_BCH) {
         HIP_OK(bchk_encode(&h->bch, d_data, ds, d_par, ps, count, h->gpu.num_cu, s));
+    } else if (h->fast && count == 1 && size <= 223) { /* one codeword: 223 dependent LFSR steps are the latency */
+        HIP_OK(rsk_encode1(h->gpu.tab, d_data, d_par, (uint32_t)size, s));
     } else if (h->fast) {
         HIP_OK(rsk_encode(h->gpu.tab, d_data, ds, d_par, ps, (uint32_t)size, count, h->gpu.num_cu, s));
     } else {

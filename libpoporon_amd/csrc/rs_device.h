@@ -54,6 +54,10 @@ struct RsDevTables {
      * (rs_correct.hip), dword x * 32 + r: (exp2[x] << 8) | (s << 16) with s =
      * 128 log (x & 255), 0xFFFF for x & 255 = 0 */
     uint4 gfc[512 * 32 / 4];
+    /* encq[d * 32 + m]: log (255 = zero) of parity byte m of the one-byte
+     * message 1 followed by d zero bytes (d < 223): the LFSR is GF-linear, so
+     * one codeword's parity is sum_j data_j encq[size - 1 - j] (rs_enc1_k) */
+    uint8_t encq[223 * 32];
 };
 #define RS_Z0 200u /* zero sentinel row of gfa (rs_fast.hip) */
 
@@ -134,6 +138,11 @@ hipError_t rsk_syndrome(const RsDevTables *tab, const uint8_t *data, size_t dstr
 hipError_t rsk_syndrome_reset(const RsDevTables *tab, const uint8_t *data, size_t dstride, const uint8_t *parity,
                               size_t pstride, uint32_t size, size_t count, uint8_t *syn, uint32_t *reset, int num_cu,
                               hipStream_t stream);
+
+/* parity of one codeword of size <= 223 as the sum of the table rows encq
+ * (one workgroup): the single-call encode; same bytes as rsk_encode */
+hipError_t rsk_encode1(const RsDevTables *tab, const uint8_t *data, uint8_t *parity, uint32_t size,
+                       hipStream_t stream);
 
 /* the same for one codeword (data, parity: its bytes), by direct evaluation
  * on one workgroup: the single-call latency path; reset as above (may be NULL) */

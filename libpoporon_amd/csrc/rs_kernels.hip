@@ -544,6 +544,48 @@ extern "C" hipError_t rsk_syndrome_reset(const RsDevTables *tab, const uint8_t *
     return launch_lfsr<MODE_SYNDROME>(tab, data, dstride, parity, pstride, size, count, syn, num_cu, stream, reset);
 }
 
+/* One codeword's parity (the single-call encode, size <= 223): the LFSR of
+ * src/encode.c:120-143 is GF-linear in the message, so parity byte m is
+ * sum_j data_j Q[size-1-j]_m with Q[d] the parity of a one-byte message 1
+ * followed by d zeros (RsDevTables::encq, log form, built on the host by
+ * running that LFSR).  Thread t: byte t & 31 over j = t >> 5 (mod 8); the
+ * eight partial sums are XORed in LDS. */
+__global__ __launch_bounds__(256) void rs_enc1_k(const RsDevTables *__restrict__ T, const uint8_t *__restrict__ data,
+                                                 uint8_t *__restrict__ parity, uint32_t size)
+{
+    __shared__ uint8_t ex[512];
+    __shared__ uint8_t lg[256];
+    __shared__ uint32_t part[256];
+    const uint32_t t = threadIdx.x;
+    ex[t] = T->exp2[t];
+    ex[t + 256] = T->exp2[t + 256];
+    lg[t] = T->log[t];
+    __syncthreads();
+    const uint32_t m = t & 31u;
+    uint32_t acc = 0;
+    for (uint32_t j = t >> 5; j < size; j += 8) {
+        const uint32_t v = data[j], q = T->encq[(size - 1u - j) * RS_NR + m];
+        if (v && q != 255u)
+            acc ^= ex[lg[v] + q];
+    }
+    part[t] = acc;
+    __syncthreads();
+    if (t < RS_NR) {
+        uint32_t v = 0;
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+            v ^= part[t + 32u * k];
+        parity[t] = (uint8_t)v;
+    }
+}
+
+extern "C" hipError_t rsk_encode1(const RsDevTables *tab, const uint8_t *data, uint8_t *parity, uint32_t size,
+                                  hipStream_t stream)
+{
+    hipLaunchKernelGGL(rs_enc1_k, dim3(1), dim3(256), 0, stream, tab, data, parity, size);
+    return hipGetLastError();
+}
+
 /* One codeword's syndromes by direct evaluation (the single-call path, where
  * the LFSR's 255 dependent steps on one lane are the latency): S_i =
  * sum_j w_j beta_i^(L-1-j), w = data || parity, L = size + 32, beta_i =
