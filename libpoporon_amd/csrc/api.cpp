@@ -136,6 +136,10 @@ struct GpuCtx {
      * one D2H copy */
     uint8_t *stage = nullptr;
     uint8_t *hstage = nullptr;
+    /* single-call encode without copies: 256 + 32 bytes of fine-grained
+     * (coherent, GPU-uncached) host memory the kernel reads and writes
+     * directly; zc_dev is its device address, NULL if unavailable */
+    uint8_t *zc = nullptr, *zc_dev = nullptr;
     size_t stage_cap = 0;
     /* host-batch pipeline: PIPE_SLOTS chunks in flight, one stream each */
     struct PipeSlot {
@@ -705,7 +709,7 @@ EXPORT poporon_t *poporon_create(const poporon_config_t *config)
 static void gpu_release(GpuCtx &g)
 {
     const int dev = g.device;
-    const bool any = g.ready || g.stream || g.tab || g.gtab || g.rem || g.stage || g.hstage || g.rem_done ||
+    const bool any = g.ready || g.stream || g.tab || g.gtab || g.rem || g.stage || g.hstage || g.zc || g.rem_done ||
                      g.pipe[0].stream || g.pipe[1].stream || g.pipe[2].stream;
     if (!any || dev < 0) {
         g = GpuCtx();
@@ -733,6 +737,8 @@ static void gpu_release(GpuCtx &g)
     (void)hipFree(g.stage);
     if (g.hstage)
         (void)hipHostFree(g.hstage);
+    if (g.zc)
+        (void)hipHostFree(g.zc);
     for (auto &ps : g.pipe) {
         if (ps.stream)
             (void)hipStreamSynchronize(ps.stream);
@@ -1778,6 +1784,27 @@ EXPORT bool poporon_encode(poporon_t *h, uint8_t *data, size_t size, uint8_t *pa
     const size_t off_p = (size + 15) & ~(size_t)15;
     if (!ensure_stage(h, off_p + nr + 16))
         return false;
+    /* one RS codeword: rs_enc1_k reads the message from and writes the
+     * parity to coherent host memory, no copies (a launch and a sync) */
+    if (h->fec_type == PPLN_FEC_RS && h->fast && size >= 1 && size <= 223) {
+        if (!g.zc) {
+            void *dp = nullptr;
+            if (hipHostMalloc((void **)&g.zc, 256 + RS_NR, hipHostMallocCoherent) == hipSuccess &&
+                hipHostGetDevicePointer(&dp, g.zc, 0) == hipSuccess)
+                g.zc_dev = (uint8_t *)dp;
+            else
+                (void)hipGetLastError(); /* unavailable: the copy path below */
+        }
+        if (g.zc_dev) {
+            memcpy(g.zc, data, size);
+            KernelTimer t(g, POPORON_AMD_KERNEL_ENCODE, g.stream);
+            HIP_OK(rsk_encode1(g.tab, g.zc_dev, g.zc_dev + 256, (uint32_t)size, g.stream));
+            t.done();
+            HIP_OK(hipStreamSynchronize(g.stream));
+            memcpy(parity, g.zc + 256, nr);
+            return true;
+        }
+    }
     /* pinned mirror: one H2D copy in, one D2H copy out */
     if (size) {
         memcpy(g.hstage, data, size);

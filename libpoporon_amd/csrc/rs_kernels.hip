@@ -555,16 +555,19 @@ __global__ __launch_bounds__(256) void rs_enc1_k(const RsDevTables *__restrict__
 {
     __shared__ uint8_t ex[512];
     __shared__ uint8_t lg[256];
+    __shared__ uint8_t msg[256];
     __shared__ uint32_t part[256];
     const uint32_t t = threadIdx.x;
     ex[t] = T->exp2[t];
     ex[t + 256] = T->exp2[t + 256];
     lg[t] = T->log[t];
+    if (t < size) /* one load per byte, all in flight together (data may be host memory) */
+        msg[t] = data[t];
     __syncthreads();
     const uint32_t m = t & 31u;
     uint32_t acc = 0;
     for (uint32_t j = t >> 5; j < size; j += 8) {
-        const uint32_t v = data[j], q = T->encq[(size - 1u - j) * RS_NR + m];
+        const uint32_t v = msg[j], q = T->encq[(size - 1u - j) * RS_NR + m];
         if (v && q != 255u)
             acc ^= ex[lg[v] + q];
     }
