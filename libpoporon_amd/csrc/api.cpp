@@ -1109,13 +1109,14 @@ static bool launch_encode(poporon_t *h, const uint8_t *d_data, size_t ds, uint8_
 /* the split error-mode decode of one sub-batch (rs_fast.hip) */
 static bool launch_split(poporon_t *h, const RsCorrParams &prm, const RsSplitWs &ws, uint8_t *d_data, size_t ds,
                          uint8_t *d_par, size_t ps, size_t size, size_t count, uint8_t *ok, uint8_t *corrected,
-                         hipStream_t s)
+                         hipStream_t s, const uint8_t *src1)
 {
     GpuCtx &g = h->gpu;
     {
         KernelTimer t(g, POPORON_AMD_KERNEL_REMAINDER, s);
         if (count == 1)
-            HIP_OK(rsk_syndrome1(g.tab, prm.fcr, prm.prim, d_data, d_par, (uint32_t)size, ws.syn, ws.nlist, s));
+            HIP_OK(rsk_syndrome1(g.tab, prm.fcr, prm.prim, src1 ? src1 : d_data, src1 ? src1 + size : d_par,
+                                 (uint32_t)size, ws.syn, ws.nlist, src1 ? d_data : nullptr, d_par, s));
         else
             HIP_OK(rsk_syndrome_reset(g.tab, d_data, ds, d_par, ps, (uint32_t)size, count, ws.syn, ws.nlist,
                                       g.num_cu, s));
@@ -1151,11 +1152,15 @@ static bool launch_split(poporon_t *h, const RsCorrParams &prm, const RsSplitWs 
 }
 
 /* rem / rem_cap: a workspace of rs_ws_bytes(rem_cap) bytes (rem_cap >= count)
- * owned by the caller; NULL: the handle's own */
+ * owned by the caller; NULL: the handle's own.  src1 (count 1, plain decode
+ * of a fast handle): the codeword's [data | parity] at a device-visible
+ * address (coherent host memory), copied to d_data / d_par by the syndrome
+ * kernel instead of a separate copy */
 static bool launch_decode(poporon_t *h, uint8_t *d_data, size_t ds, uint8_t *d_par, size_t ps, size_t size,
                           size_t count, const uint16_t *ext_syn, size_t ext_stride, const uint8_t *pos8,
                           const uint32_t *pos32, size_t pos_stride, const uint8_t *cnt, uint8_t *ok,
-                          uint8_t *corrected, hipStream_t s, uint8_t *rem = nullptr, size_t rem_cap = 0)
+                          uint8_t *corrected, hipStream_t s, uint8_t *rem = nullptr, size_t rem_cap = 0,
+                          const uint8_t *src1 = nullptr)
 {
     if (h->fec_type == PPLN_FEC_BCH) {
         if (ext_syn || pos8 || pos32)
@@ -1175,6 +1180,8 @@ static bool launch_decode(poporon_t *h, uint8_t *d_data, size_t ds, uint8_t *d_p
         t.done();
         return true;
     }
+    if (src1 && (ext_syn || pos8 || pos32 || count != 1))
+        return fail("internal: a host-side source serves one plain codeword");
     RsCorrParams prm = h->corr;
     prm.size = (uint32_t)size;
     prm.pad = (int32_t)(h->rs->gf->field_size - h->rs->num_roots - size);
@@ -1193,7 +1200,7 @@ static bool launch_decode(poporon_t *h, uint8_t *d_data, size_t ds, uint8_t *d_p
         /* (sub-batches of 2^19 codewords, to keep a sub-batch's bytes in the
          * Infinity Cache until the apply, measured slower: 0.84 vs 0.75 ms
          * per bench step) */
-        if (!launch_split(h, prm, ws, d_data, ds, d_par, ps, size, count, ok, corrected, s))
+        if (!launch_split(h, prm, ws, d_data, ds, d_par, ps, size, count, ok, corrected, s, src1))
             return false;
         return !shared || rem_release(g, s);
     }
@@ -1247,7 +1254,8 @@ static bool launch_decode(poporon_t *h, uint8_t *d_data, size_t ds, uint8_t *d_p
     if (!ext_syn) {
         KernelTimer t(h->gpu, POPORON_AMD_KERNEL_REMAINDER, s);
         if (count == 1) /* one codeword: the LFSR's 255 dependent steps are the latency */
-            HIP_OK(rsk_syndrome1(h->gpu.tab, prm.fcr, prm.prim, d_data, d_par, (uint32_t)size, rem, nullptr, s));
+            HIP_OK(rsk_syndrome1(h->gpu.tab, prm.fcr, prm.prim, src1 ? src1 : d_data, src1 ? src1 + size : d_par,
+                                 (uint32_t)size, rem, nullptr, src1 ? d_data : nullptr, d_par, s));
         else
             HIP_OK(rsk_syndrome(h->gpu.tab, d_data, ds, d_par, ps, (uint32_t)size, count, rem, h->gpu.num_cu, s));
         t.done();
@@ -1766,6 +1774,21 @@ EXPORT bool poporon_decode_batch_multi_device(poporon_multi_t *m, uint8_t *const
 /* single-codeword API (the reference's entry points): a batch of one       */
 /* ------------------------------------------------------------------------ */
 
+/* the coherent host buffer of the single-call paths (GpuCtx::zc); false if
+ * the device cannot address it (then the copy paths run) */
+static bool ensure_zc(GpuCtx &g)
+{
+    if (!g.zc) {
+        void *dp = nullptr;
+        if (hipHostMalloc((void **)&g.zc, 256 + RS_NR, hipHostMallocCoherent) == hipSuccess &&
+            hipHostGetDevicePointer(&dp, g.zc, 0) == hipSuccess)
+            g.zc_dev = (uint8_t *)dp;
+        else
+            (void)hipGetLastError();
+    }
+    return g.zc_dev != nullptr;
+}
+
 EXPORT bool poporon_encode(poporon_t *h, uint8_t *data, size_t size, uint8_t *parity)
 {
     if (!h || !data || !parity)
@@ -1787,15 +1810,7 @@ EXPORT bool poporon_encode(poporon_t *h, uint8_t *data, size_t size, uint8_t *pa
     /* one RS codeword: rs_enc1_k reads the message from and writes the
      * parity to coherent host memory, no copies (a launch and a sync) */
     if (h->fec_type == PPLN_FEC_RS && h->fast && size >= 1 && size <= 223) {
-        if (!g.zc) {
-            void *dp = nullptr;
-            if (hipHostMalloc((void **)&g.zc, 256 + RS_NR, hipHostMallocCoherent) == hipSuccess &&
-                hipHostGetDevicePointer(&dp, g.zc, 0) == hipSuccess)
-                g.zc_dev = (uint8_t *)dp;
-            else
-                (void)hipGetLastError(); /* unavailable: the copy path below */
-        }
-        if (g.zc_dev) {
+        if (ensure_zc(g)) {
             memcpy(g.zc, data, size);
             KernelTimer t(g, POPORON_AMD_KERNEL_ENCODE, g.stream);
             HIP_OK(rsk_encode1(g.tab, g.zc_dev, g.zc_dev + 256, (uint32_t)size, g.stream));
@@ -1912,12 +1927,21 @@ EXPORT bool poporon_decode(poporon_t *h, uint8_t *data, size_t size, uint8_t *pa
             pos32 = (const uint32_t *)(g.stage + off_x);
             cnt = g.stage + off_x + nr * 4;
         }
+        /* plain decode of a fast handle: the syndrome kernel reads the
+         * codeword from coherent host memory and copies it to the stage (one
+         * copy fewer on the critical path) */
+        const bool zc = !ext && !pos32 && h->fast && ensure_zc(g);
         if (refuse) {
             fail("erasure count > num_roots or external syndrome > field size: undefined in the reference, refused");
         } else {
-            HIP_OK(hipMemcpyAsync(g.stage, hs, in_bytes, hipMemcpyHostToDevice, g.stream));
+            if (zc) {
+                memcpy(g.zc, data, size);
+                memcpy(g.zc + size, parity, nr);
+            } else {
+                HIP_OK(hipMemcpyAsync(g.stage, hs, in_bytes, hipMemcpyHostToDevice, g.stream));
+            }
             if (!launch_decode(h, g.stage, size, g.stage + off_p, nr, size, 1, ext, nr, nullptr, pos32, nr, cnt,
-                               g.stage + off_ok, g.stage + off_cor, g.stream))
+                               g.stage + off_ok, g.stage + off_cor, g.stream, nullptr, 0, zc ? g.zc_dev : nullptr))
                 return false;
             HIP_OK(hipMemcpyAsync(hs, g.stage, off_cor + 1, hipMemcpyDeviceToHost, g.stream));
             HIP_OK(hipStreamSynchronize(g.stream));

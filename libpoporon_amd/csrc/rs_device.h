@@ -145,9 +145,11 @@ hipError_t rsk_encode1(const RsDevTables *tab, const uint8_t *data, uint8_t *par
                        hipStream_t stream);
 
 /* the same for one codeword (data, parity: its bytes), by direct evaluation
- * on one workgroup: the single-call latency path; reset as above (may be NULL) */
+ * on one workgroup: the single-call latency path; reset as above (may be
+ * NULL); dst_data / dst_parity (may be NULL): copy the codeword there */
 hipError_t rsk_syndrome1(const RsDevTables *tab, uint32_t fcr, uint32_t prim, const uint8_t *data,
-                         const uint8_t *parity, uint32_t size, uint8_t *syn, uint32_t *reset, hipStream_t stream);
+                         const uint8_t *parity, uint32_t size, uint8_t *syn, uint32_t *reset, uint8_t *dst_data,
+                         uint8_t *dst_parity, hipStream_t stream);
 
 /* poly syndromes (32 B per codeword, rsk_syndrome) -> log form: out[c*stride + i]
  * = log S_i (255 = zero), flag[c] = any S_i nonzero; out / flag may be NULL */

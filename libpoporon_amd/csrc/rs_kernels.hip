@@ -593,29 +593,43 @@ extern "C" hipError_t rsk_encode1(const RsDevTables *tab, const uint8_t *data, u
  * the LFSR's 255 dependent steps on one lane are the latency): S_i =
  * sum_j w_j beta_i^(L-1-j), w = data || parity, L = size + 32, beta_i =
  * alpha^(prim (fcr + i)) -- the field elements of src/decode.c:375-415 and of
- * the remainder kernel.  Thread t: syndrome t & 31 over bytes j = t >> 5
- * (mod 8); the eight partial sums are XORed in LDS. */
+ * the remainder kernel.  The codeword is staged in LDS with one load per
+ * byte (the source may be host memory; with dst_data the bytes are also
+ * copied there, for the correction kernel).  Thread t: syndrome t & 31 over
+ * bytes j = t >> 5 (mod 8); the eight partial sums are XORed in LDS. */
 __global__ __launch_bounds__(256) void rs_syn1_k(const RsDevTables *__restrict__ T, uint32_t fcr, uint32_t prim,
-                                                 const uint8_t *__restrict__ data, const uint8_t *__restrict__ parity,
-                                                 uint32_t size, uint8_t *__restrict__ syn, uint32_t *__restrict__ reset)
+                                                 const uint8_t *data, const uint8_t *parity, uint32_t size,
+                                                 uint8_t *__restrict__ syn, uint32_t *__restrict__ reset,
+                                                 uint8_t *dst_data, uint8_t *dst_parity)
 {
     __shared__ uint8_t ex[512];
     __shared__ uint8_t lg[256];
+    __shared__ uint8_t w[256];
     __shared__ uint32_t part[256];
-    const uint32_t t = threadIdx.x;
+    const uint32_t t = threadIdx.x, L = size + RS_NR;
     ex[t] = T->exp2[t];
     ex[t + 256] = T->exp2[t + 256];
     lg[t] = T->log[t];
+    if (t < L) {
+        const uint8_t v = t < size ? data[t] : parity[t - size];
+        w[t] = v;
+        if (dst_data) {
+            if (t < size)
+                dst_data[t] = v;
+            else
+                dst_parity[t - size] = v;
+        }
+    }
     if (reset && t == 0)
         *reset = 0;
     __syncthreads();
-    const uint32_t i = t & 31u, L = size + RS_NR;
+    const uint32_t i = t & 31u;
     const uint32_t b = (prim * (fcr + i)) % 255u;
     uint32_t acc = 0;
     for (uint32_t j = t >> 5; j < L; j += 8) {
-        const uint32_t w = j < size ? data[j] : parity[j - size];
-        if (w)
-            acc ^= ex[lg[w] + (b * (L - 1u - j)) % 255u];
+        const uint32_t v = w[j];
+        if (v)
+            acc ^= ex[lg[v] + (b * (L - 1u - j)) % 255u];
     }
     part[t] = acc;
     __syncthreads();
@@ -630,9 +644,10 @@ __global__ __launch_bounds__(256) void rs_syn1_k(const RsDevTables *__restrict__
 
 extern "C" hipError_t rsk_syndrome1(const RsDevTables *tab, uint32_t fcr, uint32_t prim, const uint8_t *data,
                                     const uint8_t *parity, uint32_t size, uint8_t *syn, uint32_t *reset,
-                                    hipStream_t stream)
+                                    uint8_t *dst_data, uint8_t *dst_parity, hipStream_t stream)
 {
-    hipLaunchKernelGGL(rs_syn1_k, dim3(1), dim3(256), 0, stream, tab, fcr, prim, data, parity, size, syn, reset);
+    hipLaunchKernelGGL(rs_syn1_k, dim3(1), dim3(256), 0, stream, tab, fcr, prim, data, parity, size, syn, reset,
+                       dst_data, dst_parity);
     return hipGetLastError();
 }
 
