@@ -80,8 +80,72 @@ def parse_args(argv=None):
     ap.add_argument("--no-latency", action="store_true", help="skip the single-codeword call latency")
     ap.add_argument("--backend", default="", help="tests only: module with a CPU Backend (see docstring)")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic_latest.json"),
-                    help="per-launch HBM bytes from a rocprofv3 --pmc pass")
+                    help="HBM bytes per codeword of each path from rocprofv3 --pmc passes (tools/pmc_traffic.py), "
+                         "used only when stamped with the current kernel sources")
+    ap.add_argument("--enc-copies", type=int, default=3,
+                    help="message buffers the timed encode rotates over (3 x 267 MB >= 2 x the 256 MB MALL)")
     return ap.parse_args(argv)
+
+
+# ----------------------------------------------------------------------------
+# paths (255 algorithmic bytes per codeword per mode)
+# ----------------------------------------------------------------------------
+# kernel ids of include/poporon_amd.h (POPORON_AMD_KERNEL_*) that make up each
+# mode's path; a path's time per step is the sum of its kernels' times
+K_ENCODE, K_REMAINDER, K_CORRECT, K_CHECK, K_BM, K_CHIEN, K_FORNEY, K_LIST, K_APPLY, K_ERASURE = range(10)
+PATHS = {
+    "encode": (K_ENCODE,),
+    "decode16": (K_REMAINDER, K_BM, K_CHIEN, K_FORNEY, K_APPLY, K_LIST, K_CORRECT),
+    "erasure32": (K_REMAINDER, K_ERASURE, K_LIST, K_APPLY, K_CORRECT),
+}
+
+
+def source_stamp():
+    """Hash of the product kernel sources: a PMC traffic file is used only by
+    a bench of the same kernels (tools/pmc_traffic.py writes the stamp)."""
+    import glob
+    import hashlib
+    h = hashlib.sha256()
+    csrc = os.path.join(ROOT, "libpoporon_amd", "csrc")
+    for f in sorted(glob.glob(os.path.join(csrc, "*"))):
+        if f.endswith((".hip", ".h", ".cpp")):
+            h.update(os.path.basename(f).encode())
+            with open(f, "rb") as fh:
+                h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
+def load_traffic(path):
+    """{mode: HBM bytes per codeword} from a traffic file stamped with the
+    current sources; (None, reason) otherwise."""
+    try:
+        with open(path) as f:
+            t = json.load(f)
+    except (OSError, ValueError):
+        return None, "no traffic file"
+    if t.get("source_stamp") != source_stamp():
+        return None, f"stale: traffic file stamp {t.get('source_stamp')} != kernel sources {source_stamp()}"
+    return t, None
+
+
+def path_roofline(mode, kt, steps, B, traffic):
+    """Path-level roofline of one mode: 255 B x codewords per step / the sum of
+    the mode's kernel times per step (HIP events on the launch stream)."""
+    ks = [k for k in PATHS[mode] if k in kt and kt[k][1]]
+    ms = sum(kt[k][0] / steps for k in ks)
+    if ms <= 0:
+        return None
+    achieved = B * CW_BYTES / (ms * 1e-3) / 1e9
+    r = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None, "path_ms": round(ms, 4),
+         "kernels_ms": {k: round(kt[k][0] / steps, 4) for k in ks}, "codewords": B,
+         "algorithmic_bytes": B * CW_BYTES}
+    if traffic is not None:
+        m = traffic.get("modes", {}).get(mode)
+        if m and m.get("hbm_bytes_per_cw"):
+            r["traffic"] = round(m["hbm_bytes_per_cw"] * B)
+            r["traffic_ratio"] = round(m["hbm_bytes_per_cw"] / CW_BYTES, 3)
+    return r
 
 
 # ----------------------------------------------------------------------------
@@ -319,7 +383,16 @@ def run_weak(be, ranks, args, rank, world):
     clean = be.like(cw)
     be.copy(clean, cw)
     ncopy = args.warmup + 2 * args.steps  # two timed loops (plain, then with kernel events)
-    copies = be.kind != "gpu" or ncopy * B * N <= 0.5 * be.free_bytes()
+    nenc = max(1, args.enc_copies)
+    copies = be.kind != "gpu" or (ncopy + nenc) * B * N <= 0.5 * be.free_bytes()
+    # the timed encode rotates over nenc message buffers (same messages), so
+    # no step re-encodes a buffer the Infinity Cache still holds
+    enc = [cw]
+    if copies:
+        for _ in range(nenc - 1):
+            b = be.like(cw)
+            be.copy(b, clean)
+            enc.append(b)
     bad = []
     if copies:  # one corrupted copy per step, made before the timed loop
         for _ in range(ncopy):
@@ -332,7 +405,7 @@ def run_weak(be, ranks, args, rank, world):
     def step(k):
         # the step's encode (messages in cw) and decode (a corrupted copy)
         # share no buffer: with --overlap the encode goes to a second stream
-        be.encode(cw, side=args.overlap and copies and be.kind == "gpu")
+        be.encode(enc[k % len(enc)], side=args.overlap and copies and be.kind == "gpu")
         if copies:
             d = bad[k]
         else:
@@ -364,11 +437,11 @@ def run_weak(be, ranks, args, rank, world):
         elapsed_ev = ranks.max(time.perf_counter() - t1)
         kt = {k: be.rs.timing_read(k) for k in be.P.KERNEL_NAMES}
         be.rs.timing(False)
-    nbad = be.n_bad(st, 16) + be.n_diff(cw, clean)
+    nbad = be.n_bad(st, 16) + sum(be.n_diff(b, clean) for b in enc)
     nbad += sum(be.n_diff(b, clean) for b in (bad[args.warmup:args.warmup + (2 if elapsed_ev else 1) * args.steps]
                                               if copies else [cw]))
     csum = be.checksum(cw, first)
-    del bad
+    del bad, enc
     return {"elapsed": elapsed, "elapsed_ev": elapsed_ev, "kt": kt, "nbad": ranks.sum_int(nbad), "copies": copies,
             "checksum": ranks.sum_u64(csum), "cw": cw, "clean": clean, "err": err, "st": st}
 
@@ -409,18 +482,20 @@ def run_erasure(be, ranks, args, rank, world, w):
         estep(1 + k)
     ranks.barrier(be.sync)
     et = ranks.max(time.perf_counter() - t0)
-    ekt = {be.P.KERNEL_NAMES[k]: be.rs.timing_read(k) for k in be.P.KERNEL_NAMES}
-    kms = sum(ms / n for ms, n in ekt.values() if n)
+    ekt = {k: be.rs.timing_read(k) for k in be.P.KERNEL_NAMES}
+    ekt = {k: v for k, v in ekt.items() if v[1]}
+    kms = sum(ms / es for ms, n in ekt.values())
     be.rs.timing(False)
     enbad = be.n_bad(w["st"], 32) + sum(be.n_diff(b, eclean) for b in (ebad[1:] if ecopies else [cw]))
     enbad = ranks.sum_int(enbad)
     return {"cw_per_s": round(B * world * es / et, 1),
             "kernel_cw_per_s_per_gpu": round(B / (kms * 1e-3), 1) if kms else None,
-            "kernels_avg_ms": {name: round(ms / n, 4) for name, (ms, n) in ekt.items() if n},
+            "kernels_avg_ms": {be.P.KERNEL_NAMES[k]: round(ms / n, 4) for k, (ms, n) in ekt.items()},
             "positions_bytes_per_cw": 32,
             "verified": enbad == 0,
             "channel": "outside the timed decodes (one corrupted copy per decode)" if ecopies
-            else "in place, inside the timed decodes"}
+            else "in place, inside the timed decodes",
+            "_kt": ekt, "_steps": es}
 
 
 # ----------------------------------------------------------------------------
@@ -663,37 +738,52 @@ def main(argv=None):
         per_kernel = {}
         # a kernel may run several times per step (the split decode works in
         # sub-batches): per-step time = total / steps, codewords per launch =
-        # B * steps / launches
+        # B * steps / launches.  No per-kernel GB/s: the 255 algorithmic bytes
+        # belong to a mode's whole path, not to one of its stages.
         step_ms = {k: ms / args.steps for k, (ms, n) in kt.items()}
         avg_ms = {k: ms / n for k, (ms, n) in kt.items()}
         per_launch = {k: B * args.steps / n for k, (ms, n) in kt.items()}
+        traffic, tnote = load_traffic(args.traffic)
         for k, (ms, n) in kt.items():
             per_kernel[P.KERNEL_NAMES[k]] = {"ms_per_step": round(step_ms[k], 4), "avg_ms": round(avg_ms[k], 4),
                                              "launches": n, "codewords_per_launch": int(per_launch[k]),
-                                             "cw_per_s_per_gpu": round(B / (step_ms[k] * 1e-3), 1),
-                                             "GB_s_algorithmic": round(B * CW_BYTES / (step_ms[k] * 1e-3) / 1e9, 1)}
+                                             "cw_per_s_per_gpu": round(B / (step_ms[k] * 1e-3), 1)}
         enc_ms = sum(v for k, v in step_ms.items() if k == P.KERNEL_ENCODE)
         dec_ms = sum(v for k, v in step_ms.items() if k != P.KERNEL_ENCODE)
-        dom = max(kt, key=lambda k: kt[k][0])
-        achieved = per_launch[dom] * CW_BYTES / (avg_ms[dom] * 1e-3) / 1e9
-        traffic = None
-        try:
-            with open(args.traffic) as f:
-                traffic = json.load(f).get("kernels", {}).get(P.KERNEL_NAMES[dom], {}).get("hbm_bytes_per_launch")
-        except (OSError, ValueError):
-            pass
+        modes = {"encode": path_roofline("encode", kt, args.steps, B, traffic),
+                 "decode16": path_roofline("decode16", kt, args.steps, B, traffic)}
+        if not args.no_erasure:
+            era = run_erasure(be, ranks, args, rank, world, w)
+            modes["erasure32"] = path_roofline("erasure32", era.pop("_kt"), era.pop("_steps"), B, traffic)
+            line["erasure_decode_32"] = era
+            line["verified"] = line["verified"] and era["verified"]
+        rt_ms = modes["encode"]["path_ms"] + modes["decode16"]["path_ms"]
+        rt = 2 * B * CW_BYTES / (rt_ms * 1e-3) / 1e9
+        modes["roundtrip"] = {"achieved": round(rt, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                              "frac": round(rt / HBM_PEAK_GBS, 4), "path_ms": round(rt_ms, 4),
+                              "algorithmic_bytes": 2 * B * CW_BYTES,
+                              "traffic": (modes["encode"]["traffic"] + modes["decode16"]["traffic"]
+                                          if modes["encode"]["traffic"] and modes["decode16"]["traffic"] else None),
+                              "note": "encode path + decode16 path, 255 B per codeword per mode"}
+        roof = dict(modes["decode16"])
+        roof.update({"kernel": "decode16 path (" + " + ".join(P.KERNEL_NAMES[k] for k in roof["kernels_ms"]) + ")",
+                     "note": "path-level: 255 B x codewords / sum of the path's kernel times per step (HIP events "
+                             "on the launch stream); traffic = HBM bytes of the same path from rocprofv3 "
+                             "FETCH_SIZE x 2 + WRITE_SIZE (tools/pmc_traffic.py); the kernels are VALU/LDS-bound, "
+                             "see DESIGN.md"})
+        roof["kernels_ms"] = {P.KERNEL_NAMES[k]: v for k, v in roof["kernels_ms"].items()}
+        for m in modes.values():
+            if "kernels_ms" in m:
+                m["kernels_ms"] = {P.KERNEL_NAMES.get(k, k): v for k, v in m["kernels_ms"].items()}
         line.update({
             "encode_cw_per_s_per_gpu": round(B / (enc_ms * 1e-3), 1),
             "decode_cw_per_s_per_gpu": round(B / (dec_ms * 1e-3), 1),
             "kernels": per_kernel,
-            "roofline": {"kernel": P.KERNEL_NAMES[dom], "bound": "hbm", "achieved": round(achieved, 1),
-                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                         "traffic": traffic,
-                         "note": "achieved = 255 B x codewords per launch / average launch time (HIP events, "
-                                 "launch stream); the kernel is VALU/LDS-bound, see DESIGN.md"},
+            "roofline": roof,
+            "roofline_modes": modes,
+            "traffic_source": (f"{args.traffic} (stamp {traffic.get('source_stamp')}, measured {traffic.get('date')})"
+                               if traffic else tnote),
         })
-        if not args.no_erasure:
-            line["erasure_decode_32"] = run_erasure(be, ranks, args, rank, world, w)
         if world == 1 and not args.no_host:
             line["host_pipeline"] = host_pipeline(be, w)
         if world == 1 and not args.no_latency:

@@ -517,8 +517,6 @@ static void build_tables(poporon_t *h)
         }
     const char *fv = getenv("POPORON_AMD_FORCE_VERIFY");
     p.force_verify = (fv && fv[0] == '1') ? 1u : 0u;
-    const char *sa = getenv("POPORON_AMD_STOP_AT"); /* profiling ablation only */
-    p.stop_at = sa ? (uint32_t)atoi(sa) : 0u;
     const char *dp = getenv("POPORON_AMD_DECODE_PATH");
     h->decode_path = dp && !strcmp(dp, "split") ? 1 : (dp && !strcmp(dp, "single") ? 2 : 0);
 }
@@ -1137,7 +1135,7 @@ static bool launch_split(poporon_t *h, const RsCorrParams &prm, const RsSplitWs 
         HIP_OK(rsk_forney(g.tab, &prm, &ws, d_data, ds, d_par, ps, count, ok, corrected, g.num_cu, s));
         t.done();
     }
-    if (prm.stop_at != 5u) { /* 5: profiling ablation, no apply */
+    {
         KernelTimer t(g, POPORON_AMD_KERNEL_APPLY, s);
         HIP_OK(rsk_apply(&prm, &ws, d_data, ds, d_par, ps, count, s));
         t.done();
@@ -1192,7 +1190,7 @@ static bool launch_decode(poporon_t *h, uint8_t *d_data, size_t ds, uint8_t *d_p
         rem = h->gpu.rem;
         rem_cap = h->gpu.rem_cap;
     }
-    const bool split = !ext_syn && !pos8 && !pos32 && prm.vfast && !prm.force_verify && (!prm.stop_at || prm.stop_at >= 5) &&
+    const bool split = !ext_syn && !pos8 && !pos32 && prm.vfast && !prm.force_verify &&
                        h->decode_path != 2 && (h->decode_path == 1 || count >= SPLIT_MIN_COUNT);
     if (split) {
         const RsSplitWs ws = rs_ws_carve(rem, rem_cap ? rem_cap : count);
@@ -1207,7 +1205,7 @@ static bool launch_decode(poporon_t *h, uint8_t *d_data, size_t ds, uint8_t *d_p
     /* erasure batches: the general kernel's decode with the corrections as
      * records, applied block-wise (scattered byte read-modify-writes cost
      * ~0.3 ms per 2^20 codewords with 32 erasures) */
-    const bool esplit = !ext_syn && (pos8 || pos32) && prm.vfast && !prm.force_verify && !prm.stop_at &&
+    const bool esplit = !ext_syn && (pos8 || pos32) && prm.vfast && !prm.force_verify &&
                         h->decode_path != 2 && (h->decode_path == 1 || count >= SPLIT_MIN_COUNT);
     if (esplit) {
         const RsSplitWs ws = rs_ws_carve(rem, rem_cap ? rem_cap : count);
@@ -1920,8 +1918,8 @@ EXPORT bool poporon_decode(poporon_t *h, uint8_t *data, size_t size, uint8_t *pa
              * slots, those past the list's capacity read as 0 */
             memset(hs + off_x, 0, nr * 4);
             memcpy(hs + off_x, e->erasure_positions, std::min<size_t>(e->capacity, nr) * sizeof(uint32_t));
-            if (e->erasure_count > nr)
-                refuse = true; /* quirk Q5: overflows the locator in the reference */
+            /* counts past num_roots (quirk Q5) reach the kernel as they are
+             * (clamped to 255): refused there only for a dirty codeword */
             hs[off_x + nr * 4] = (uint8_t)std::min<uint32_t>(e->erasure_count, 255u);
             in_bytes = off_x + nr * 4 + 1;
             pos32 = (const uint32_t *)(g.stage + off_x);
@@ -1932,7 +1930,7 @@ EXPORT bool poporon_decode(poporon_t *h, uint8_t *data, size_t size, uint8_t *pa
          * copy fewer on the critical path) */
         const bool zc = !ext && !pos32 && h->fast && ensure_zc(g);
         if (refuse) {
-            fail("erasure count > num_roots or external syndrome > field size: undefined in the reference, refused");
+            fail("external syndrome > field size: undefined in the reference, refused");
         } else {
             if (zc) {
                 memcpy(g.zc, data, size);

@@ -57,12 +57,8 @@
 #define COR_WG 1024
 #define GF_REPL 32
 #define A0 RS_A0
-#ifndef BM_DISC_G
 #define BM_DISC_G 8 /* BM discrepancy terms per branch-free group */
-#endif
-#ifndef FORNEY_R
 #define FORNEY_R 4  /* Forney/apply: roots per step (their sums and byte loads overlap) */
-#endif
 #define ZL 1024u         /* log of zero (registers): exp(ZL + anything) reads past the LDS block -> 0 */
 #define BIG 0x10000000u  /* log of zero in the Chien index walk (survives 255 reductions, clamped to 255) */
 
@@ -225,9 +221,6 @@ __device__ __forceinline__ bool correct_one(const Gf &gf, const uint4 *__restric
         ll[i] = l < 255u ? l : ZL;
     }
 
-    if (P.stop_at == 2u)
-        return dl > 40u; /* profiling ablation */
-
     /* ---- degree, src/decode.c:98-110 ---- */
     uint32_t deg = 0;
 #pragma unroll
@@ -272,9 +265,6 @@ __device__ __forceinline__ bool correct_one(const Gf &gf, const uint4 *__restric
     else
         omega(std::integral_constant<int, 0>{});
 #define OMLOG(m) (((m) & 1) ? (omp[(m) >> 1] >> 16) : (omp[(m) >> 1] & 0xffffu))
-    if (P.stop_at == 3u)
-        return omp[0] > 3000u; /* profiling ablation */
-
     /* derivative terms (Forney, below): Lambda_(2h+1) for 2h <= min(deg, 31) (src/decode.c:176-180);
      * those with 2h + 1 > deg are zero, so the terms stop at 2h <= deg - 1
      * (16 errors: 8 terms, and Forney's powers stop at m < 16, not 17) */
@@ -398,9 +388,6 @@ __device__ __forceinline__ bool correct_one(const Gf &gf, const uint4 *__restric
         cnt += __popc(rb[w]);
     if (cnt != deg)
         return false; /* src/decode.c:143-145 */
-    if (P.stop_at == 4u)
-        return false; /* profiling ablation */
-
     /* locations k = (i*iprim - 1) mod 255 below pad fail, src/decode.c:132-134 */
     if (pad > 0) {
         RootIter it;
@@ -772,7 +759,15 @@ __global__ __launch_bounds__(COR_WG) void rs_correct_k(const RsDevTables *__rest
             sw[4] = sb.x, sw[5] = sb.y, sw[6] = sb.z, sw[7] = sb.w;
         }
         const uint32_t ne0 = (ERA && valid) ? cnt[cw] : 0u;
-        const bool refuse = ne0 > RS_NR || ext_bad; /* undefined behaviour in the reference (quirk Q5): refused */
+        /* a clean codeword succeeds whatever its erasure count (src/decode.c:468:
+         * the syndrome test comes first); a dirty one with more erasures than
+         * roots overflows the reference's locator (quirk Q5): refused, as
+         * rs_era_k does */
+        bool dirty = false;
+#pragma unroll
+        for (int q = 0; q < RS_NR / 4; ++q)
+            dirty |= syn16 ? sw[q] != 0xFFFFFFFFu : sw[q] != 0u;
+        const bool refuse = (ne0 > RS_NR && dirty) || ext_bad;
         bool any = false;
 #pragma unroll
         for (uint32_t q = 0; q < RS_NR; ++q) {
@@ -781,7 +776,7 @@ __global__ __launch_bounds__(COR_WG) void rs_correct_k(const RsDevTables *__rest
             any |= lv != A0;
             srow[(31u - q) * COR_WG] = (uint8_t)lv;
         }
-        const bool need = any && P.stop_at != 1u;
+        const bool need = any;
         const size_t cs = valid ? cw : 0; /* rows of lanes past the batch: a mapped row, never written */
         uint32_t fixed = 0;
         bool good = !refuse;
@@ -838,9 +833,9 @@ extern "C" hipError_t rsk_correct_list(const RsDevTables *tab, const RsCorrParam
 {
     if (count == 0)
         return hipSuccess;
-    /* the list is empty for codewords with at most 16 errors: a small grid
-     * leaves quickly (each block loops over the list when it is long) */
-    const dim3 grid(std::min(persistent_grid(count, COR_WG, num_cu), 64));
+    /* full persistent grid: the list is empty for codewords with at most 16
+     * errors, and blocks past its length leave before filling their tables */
+    const dim3 grid(persistent_grid(count, COR_WG, num_cu));
     hipLaunchKernelGGL((rs_correct_k<uint8_t, false>), grid, dim3(COR_WG), 0, stream, tab, *prm, data, dstride,
                        parity, pstride, count, syn, nullptr, 0, nullptr, 0, nullptr, ok, corrected, list, list_n);
     return hipGetLastError();

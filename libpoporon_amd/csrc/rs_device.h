@@ -73,9 +73,6 @@ struct RsCorrParams {
     int32_t pad;     /* 255 - 32 - size */
     uint32_t vfast;  /* (fcr+31)*prim*254 < 32768: verification exponents need no int16 emulation */
     uint32_t force_verify; /* run the re-syndrome check even where it provably passes (tests) */
-    uint32_t stop_at;      /* profiling only (stage ablation): 0 = full decode; 1/2/3/4 = return
-                              after syndrome load / erasure+BM / Omega / Chien (results invalid);
-                              5 = split decode without the apply */
     uint8_t tr_start[RS_NR];
     uint8_t tr_inc[RS_NR];
 };

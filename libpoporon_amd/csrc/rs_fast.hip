@@ -55,18 +55,9 @@
 #define NL 17          /* Lambda_0..16 and B_0..16: t = 16 */
 #define Z0 RS_Z0       /* zero sentinels: AZ = 128 Z0 + 4r, SZ = 128 Z0 - 1 (see the header) */
 #define SZ (128u * Z0 - 1u)
-#ifndef FORNEY_R
 #define FORNEY_R 1     /* roots per Forney step (more spill at 64 VGPRs) */
-#endif
-#ifndef FORNEY_WAVES
 #define FORNEY_WAVES 8
-#endif
-#ifndef APPLY_REV
-#define APPLY_REV 1
-#endif
-#ifndef BM_WAVES
 #define BM_WAVES 8
-#endif
 
 /* ------------------------------------------------------------------------ */
 /* GF table (rs_bm_k, rs_forney_k)                                          */
@@ -334,163 +325,6 @@ __global__ __launch_bounds__(FWG, BM_WAVES) void rs_bm_k(const RsDevTables *__re
 }
 
 
-/* ------------------------------------------------------------------------ */
-/* rs_bm16_k: the north_star mapping -- sixteen lanes per codeword          */
-/* ------------------------------------------------------------------------ */
-
-/*
- * Berlekamp-Massey with the codeword spread over a 16-lane DPP row (four
- * codewords per wave): lane k holds Lambda_(k+1) (poly and address-form log)
- * and B_k (address-form log), so the update Lambda_(k+1) += q B_k is lane
- * local; the discrepancy is one lookup per lane (Lambda_(k+1) S_(r-2-k), a
- * sliding syndrome window moved by row_shr:1) reduced over the row with four
- * DPP xors, plus S_(r-1) broadcast by ds_swizzle; B <- x Lambda_old / x B is
- * a row_shr:1.  Omega_m is lane m's sum over broadcast Lambda_j.  Address-form
- * logs carry their lane's replica offset (4 (lane & 31) + 1): moved one lane
- * up they gain 4.  Same outputs as rs_bm_k (measurement of the mapping,
- * BM_GROUP=1; profiles/r02_bm_group_experiment.log).
- */
-#ifndef BM_GROUP
-#define BM_GROUP 0
-#endif
-#if BM_GROUP
-__device__ __forceinline__ uint32_t dpp_shr1(uint32_t v) /* lane k of a row <- lane k-1, lane 0 <- 0 */
-{
-    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, true);
-}
-template <int CTRL> __device__ __forceinline__ uint32_t dpp_x(uint32_t v)
-{
-    return v ^ (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, 0xf, 0xf, false);
-}
-/* xor over the 16 lanes of a row, in every lane */
-__device__ __forceinline__ uint32_t row_xor(uint32_t v)
-{
-    v = dpp_x<0xB1>(v);  /* quad_perm [1,0,3,2] */
-    v = dpp_x<0x4E>(v);  /* quad_perm [2,3,0,1] */
-    v = dpp_x<0x124>(v); /* row_ror:4 */
-    return dpp_x<0x128>(v); /* row_ror:8 */
-}
-/* lane J of this lane's 16-lane group, via ds_swizzle (bit mode: and 0x10, or J) */
-template <int J> __device__ __forceinline__ uint32_t grp_bcast(uint32_t v)
-{
-    return (uint32_t)__builtin_amdgcn_ds_swizzle((int)v, 0x10 | (J << 5));
-}
-
-__global__ __launch_bounds__(FWG, BM_WAVES) void rs_bm16_k(const RsDevTables *__restrict__ T,
-                                                     const uint8_t *__restrict__ syn, size_t count,
-                                                     uint8_t *__restrict__ lamo, uint8_t *__restrict__ omo,
-                                                     uint8_t *__restrict__ meta, uint32_t *__restrict__ list,
-                                                     uint32_t *__restrict__ nlist, uint8_t *__restrict__ ok,
-                                                     uint8_t *__restrict__ corrected)
-{
-    __shared__ uint32_t lgf[512 * 32];
-    fill_gfa(lgf, T);
-    __syncthreads();
-    const GfA gf{lds_addr(lgf) + 4u * (threadIdx.x & 31u) + 1u};
-    const uint32_t pofs = gf.pofs, AZ = gf.az();
-    const uint32_t k = threadIdx.x & 15u;
-    const uint32_t m0 = k == 0u ? 0xFFFFFFFFu : 0u; /* lane 0 of the group */
-    const uint32_t gsh = threadIdx.x & 48u;          /* the group's bit offset in a wave ballot */
-    /* pofs of lane 0 of this lane's group (broadcast address-form logs are rebased from it) */
-    const uint32_t g0pofs = 4u * ((threadIdx.x & 16u)) + 1u;
-
-    for (size_t base = (size_t)blockIdx.x * (FWG / 16); base < count; base += (size_t)gridDim.x * (FWG / 16)) {
-        const size_t cw = base + (threadIdx.x >> 4);
-        const bool valid = cw < count;
-        uint32_t s_lo = 0, s_hi = 0; /* S_k, S_(k+16) */
-        if (valid) {
-            s_lo = syn[cw * RS_NR + k];
-            s_hi = syn[cw * RS_NR + 16 + k];
-        }
-        const uint64_t bal = __ballot((s_lo | s_hi) != 0u);
-        const bool any = ((bal >> gsh) & 0xFFFFull) != 0ull;
-        if (bal == 0ull) {
-            if (valid && k == 0u) {
-                ok[cw] = 1;
-                if (corrected)
-                    corrected[cw] = 0;
-                meta[cw] = (uint8_t)(RS_ST_DONE << 5);
-            }
-            continue;
-        }
-        const uint32_t ls_lo = gf.logs(s_lo), ls_hi = gf.logs(s_hi); /* scaled logs (SZ: zero) */
-        uint32_t P = 0, A = AZ;                  /* Lambda_(k+1) */
-        uint32_t LB = k == 0u ? pofs : AZ;       /* B_k (B = 1) */
-        uint32_t w = SZ;                         /* scaled log S_(r-2-k) */
-        uint32_t b16 = 0, L = 0, lb = 0, over = 0, bo = 0;
-        static_for<1, RS_NR + 1, 1>([&](auto rc) __attribute__((always_inline)) {
-            constexpr int r = decltype(rc)::value;
-            const uint32_t sp = grp_bcast<(r - 1) & 15>(r - 1 < 16 ? s_lo : s_hi);   /* S_(r-1) */
-            const uint32_t lsp = grp_bcast<(r - 1) & 15>(r - 1 < 16 ? ls_lo : ls_hi); /* its scaled log */
-            const uint32_t disc = row_xor(gf.expa(A + w)) ^ sp;
-            w = __builtin_amdgcn_bitop3_b32(dpp_shr1(w), lsp, m0, 0xF8); /* a | (b & c): S_(r-1-k) next */
-            const uint32_t ld = gf.logs(disc);
-            const bool upd = disc != 0u;
-            const bool lengthen = upd && (2u * L <= (uint32_t)(r - 1));
-            const int32_t dd = (int32_t)ld - (int32_t)lb;
-            const uint32_t dq = upd ? (uint32_t)(dd < 0 ? dd + 255 * 128 : dd) : SZ;
-            over |= upd ? (bo | b16) : 0u;
-            bo = lengthen ? 0u : (bo | b16);
-            /* B <- x Lambda_old (lengthening) or x B: one lane up (+4 on the address form), lane 0 <- 1 or 0 */
-            const uint32_t src = lengthen ? A : LB;
-            const uint32_t top = grp_bcast<15>(src != ((4u * ((threadIdx.x & 16u) + 15u) + 1u) + SZ) ? 1u : 0u);
-            const uint32_t lbn = __builtin_amdgcn_bitop3_b32(dpp_shr1(src) + 4u, lengthen ? pofs : AZ, m0, 0xF8);
-            P ^= gf.expa(LB + dq);
-            A = gf.loga(P);
-            LB = k == 0u ? (lengthen ? pofs : AZ) : lbn;
-            b16 = top;
-            if (lengthen) {
-                L = (uint32_t)r - L;
-                lb = ld;
-            }
-            /* the state pinned per iteration (no deferred flag chains: spills) */
-            asm volatile("" : "+v"(P), "+v"(A), "+v"(LB), "+v"(w), "+v"(b16), "+v"(L), "+v"(lb), "+v"(over), "+v"(bo));
-            __builtin_amdgcn_sched_barrier(0);
-        });
-
-        /* degree: the highest k + 1 with Lambda_(k+1) != 0, over the group */
-        const uint64_t nzb = __ballot(P != 0u);
-        const uint32_t gm = (uint32_t)((nzb >> gsh) & 0xFFFFull);
-        const uint32_t deg = gm ? 32u - __builtin_clz(gm) : 0u;
-        const bool fast = any && !over && deg == L && deg != 0u;
-
-        /* Omega_m (lane m) = sum_(j <= m) Lambda_j S_(m-j) */
-        uint32_t acc = 0, v = ls_lo; /* v: scaled log S_(m-j) */
-        static_for<0, 16, 1>([&](auto jc) __attribute__((always_inline)) {
-            constexpr int j = decltype(jc)::value;
-            uint32_t aj; /* address-form log of Lambda_j in this lane's replica */
-            if constexpr (j == 0)
-                aj = pofs;
-            else
-                aj = grp_bcast<j - 1>(A) - (g0pofs + 4u * (uint32_t)(j - 1)) + pofs;
-            acc ^= gf.expa(aj + v);
-            v = __builtin_amdgcn_bitop3_b32(dpp_shr1(v), SZ, m0, 0xF8);
-        });
-        const uint32_t om = k < deg ? gf.plog(gf.loga(acc)) : 255u;
-
-        if (valid) {
-            if (!any) {
-                if (k == 0u) {
-                    ok[cw] = 1;
-                    if (corrected)
-                        corrected[cw] = 0;
-                    meta[cw] = (uint8_t)(RS_ST_DONE << 5);
-                }
-            } else if (!fast) {
-                if (k == 0u) {
-                    meta[cw] = (uint8_t)(RS_ST_LIST << 5);
-                    list[atomicAdd(nlist, 1u)] = (uint32_t)cw;
-                }
-            } else {
-                lamo[cw * 16 + k] = (uint8_t)gf.plog(A);
-                omo[cw * 16 + k] = (uint8_t)om;
-                if (k == 0u)
-                    meta[cw] = (uint8_t)((RS_ST_FAST << 5) | deg);
-            }
-        }
-    }
-}
-#endif /* BM_GROUP */
 
 /* ------------------------------------------------------------------------ */
 /* rs_chien_k: root map                                                      */
@@ -804,13 +638,9 @@ __global__ __launch_bounds__(FWG, FORNEY_WAVES) void rs_forney_k(const RsDevTabl
  * packed two per register for Omega (16 + 16 syndrome logs + 16 Omega) and
  * Forney (Omega, odd Lambda: 24); slots are re-read where needed.
  */
-#ifndef ERA_WAVES
 #define ERA_WAVES 6 /* 80 VGPRs: 0.351 ms per 2^20 codewords; 4: 0.358, 8 (a few spills outside the loops): 0.365 */
-#endif
 #define ERA_R 4 /* Forney roots per step: one record dword */
-#ifndef ERA_OG
 #define ERA_OG 8 /* Omega lookups per group */
-#endif
 
 __global__ __launch_bounds__(FWG, ERA_WAVES) void rs_era_k(const RsDevTables *__restrict__ T, RsCorrParams P,
                                                          const uint8_t *__restrict__ syn,
@@ -1069,11 +899,8 @@ __global__ __launch_bounds__(AWG) void rs_apply_k(const uint8_t *__restrict__ me
     constexpr int NW = NC / 4; /* record dwords of positions (then as many of magnitudes) */
     __shared__ uint4 img[AWG / 64][ABLK];
     const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63u;
-#if APPLY_REV /* last blocks first: the codewords the syndrome pass read last may still sit in the MALL */
+    /* last blocks first: the codewords the syndrome pass read last may still sit in the MALL */
     const size_t base = ((size_t)(gridDim.x - 1u - blockIdx.x) * (AWG / 64) + w) * 64u;
-#else
-    const size_t base = ((size_t)blockIdx.x * (AWG / 64) + w) * 64u;
-#endif
     if (base >= count)
         return;
     const size_t cw = base + lane;
@@ -1151,16 +978,8 @@ extern "C" hipError_t rsk_bm(const RsDevTables *tab, const RsSplitWs *ws, size_t
 {
     if (count == 0)
         return hipSuccess;
-#if BM_GROUP
-    {
-        const size_t need = (count + FWG / 16 - 1) / (FWG / 16), g = 2u * (size_t)(num_cu > 0 ? num_cu : 256);
-        hipLaunchKernelGGL(rs_bm16_k, dim3((int)(need < g ? need : g)), dim3(FWG), 0, stream, tab, ws->syn, count,
-                           ws->lam, ws->om, ws->meta, ws->list, ws->nlist, ok, corrected);
-    }
-#else
     hipLaunchKernelGGL(rs_bm_k, dim3(fast_grid(count, num_cu)), dim3(FWG), 0, stream, tab, ws->syn, count, ws->lam,
                        ws->om, ws->meta, ws->list, ws->nlist, ok, corrected);
-#endif
     return hipGetLastError();
 }
 

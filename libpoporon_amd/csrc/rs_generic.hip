@@ -368,12 +368,10 @@ __global__ __launch_bounds__(G_WG_MAX) void rsg_decode_k(const RsGenTables *__re
                 fixed = 0;
         } else if (pos) {
             const uint32_t ne = cntv[cw];
-            if (ne > nr) { /* quirk Q5: overflows the locator in the reference */
-                good = false;
-            } else {
-                good = !g_syndromes(s, mod, P, d, par, S) ||
-                       g_correct<PosT>(s, mod, P, d, par, S, ne, pos + cw * pos_stride, true, fixed);
-            }
+            /* clean: success whatever the count (src/decode.c:468); dirty with
+             * ne > nr overflows the reference's locator (quirk Q5): refused */
+            const bool dirty = g_syndromes(s, mod, P, d, par, S);
+            good = !dirty || (ne <= nr && g_correct<PosT>(s, mod, P, d, par, S, ne, pos + cw * pos_stride, true, fixed));
         } else {
             good = !g_syndromes(s, mod, P, d, par, S) ||
                    g_correct<PosT>(s, mod, P, d, par, S, 0u, (const PosT *)nullptr, false, fixed);

@@ -10,11 +10,15 @@
 
 #include "rs_device.h"
 
-/* LDS reads from a byte address (address space 3, made from an integer):
- * addresses past the workgroup's allocation read 0 on gfx950 (probed:
- * tools/probes/lds_oob.hip), which the zero sentinels below rely on; going
- * through an integer keeps the compiler from reasoning about the bounds of
- * a C++ object. */
+/* LDS reads from a byte address (address space 3, made from an integer;
+ * going through an integer keeps the compiler from reasoning about the
+ * bounds of a C++ object).  What a read past the workgroup's allocation
+ * returns depends on the allocation: past the end of the whole 160 KiB LDS
+ * it reads 0 (tools/probes/lds_oob.hip), which rs_correct_k's zero sentinel
+ * relies on (its table ends exactly there: static_assert LDS_END == 163840 in
+ * rs_correct.hip); past a smaller allocation it may read another
+ * workgroup's LDS (tools/probes/lds_oob64.hip), so the split kernels keep
+ * every read inside their own tables (rs_fast.hip header). */
 typedef __attribute__((address_space(3))) const uint8_t lds_u8;
 typedef __attribute__((address_space(3))) const uint16_t lds_u16;
 typedef unsigned lds_u32x4_t __attribute__((ext_vector_type(4)));
@@ -47,24 +51,16 @@ __device__ __forceinline__ uint32_t half(const uint32_t *a, int i)
     return (i & 1) ? (a[i >> 1] >> 16) : (a[i >> 1] & 0xffffu);
 }
 
-#ifndef U16RED
-#define U16RED 1
-#endif
 /* (x + y) mod 255 * 128 for scaled logs x, y < 255 * 128: three full-rate
  * 16-bit ops instead of add, add, half-rate v_min_u32 (gfx950's VOP2 16-bit
  * ops zero bits 31:16 of the result: tools/probes/u16_hi.hip) */
 __device__ __forceinline__ uint32_t addmod7(uint32_t x, uint32_t y)
 {
-#if U16RED
     uint32_t t, u, r;
     asm("v_add_u16 %0, %1, %2" : "=v"(t) : "v"(x), "v"(y));
     asm("v_subrev_u16 %0, 0x7f80, %1" : "=v"(u) : "v"(t)); /* t - 255 * 128, wraps above t when t < 255 * 128 */
     asm("v_min_u16 %0, %1, %2" : "=v"(r) : "v"(t), "v"(u));
     return r;
-#else
-    const uint32_t t = x + y;
-    return min(t, t - 255u * 128u);
-#endif
 }
 
 /* a ^ b ^ c in one VALU op (gfx950 v_bitop3_b32, truth table 0x96) */

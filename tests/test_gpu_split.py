@@ -261,3 +261,37 @@ def test_split_erasures_other_parameters_vs_oracle(monkeypatch, params):
     want = o.decode_batch(cw[:, :223], cw[:, 223:], slots.astype(np.uint32), cnt.astype(np.uint32))
     assert want[0].sum() > 1000
     _same(got, want)
+
+
+@pytest.mark.parametrize("path", PATHS)
+def test_erasure_count_past_roots(monkeypatch, oracle_default, path):
+    """Erasure counts 33..255 (quirk Q5, undefined in the reference only once
+    the locator is built): a clean codeword succeeds with 0 corrections
+    whatever its count (src/decode.c:468 tests the syndromes first), a dirty
+    one is refused (ok 0, bytes untouched) -- the same answer on the split
+    path (rs_era_k + list) and the single kernel, mixed with in-range
+    codewords in every wave."""
+    h = _handle(monkeypatch, path)
+    rng = np.random.default_rng(4242)
+    n = 16384
+    data = rng.integers(0, 256, (n, 223), dtype=np.uint8)
+    cw = np.concatenate([data, h.encode_batch(data)], 1)
+    slots = np.zeros((n, NR), np.uint8)
+    cnt = rng.integers(33, 256, n).astype(np.uint8)
+    inr = np.arange(n) % 3 == 0  # in-range codewords: 32 sorted erasures
+    cnt[inr] = NR
+    dirty = np.arange(n) % 2 == 0
+    for c in range(n):
+        slots[c] = np.sort(rng.permutation(223)[:NR])
+        if dirty[c]:
+            cw[c, slots[c]] ^= rng.integers(1, 256, NR, dtype=np.uint8)
+    ok, cor, d, p = h.decode_batch(cw[:, :223], cw[:, 223:], slots, cnt)
+    clean_far = ~dirty & ~inr
+    dirty_far = dirty & ~inr
+    assert (ok[clean_far] == 1).all() and (cor[clean_far] == 0).all()
+    assert (ok[dirty_far] == 0).all() and (cor[dirty_far] == 0).all()
+    out = np.concatenate([d, p], 1)
+    assert (out[~inr] == cw[~inr]).all()
+    want = oracle_default.decode_batch(cw[inr, :223], cw[inr, 223:], slots[inr].astype(np.uint32),
+                                       cnt[inr].astype(np.uint32))
+    _same((ok[inr], cor[inr], d[inr], p[inr]), want)

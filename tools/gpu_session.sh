@@ -27,7 +27,7 @@ for step in "$@"; do
     tests_all) run tests_all 900 python -m pytest tests -m gpu -q ;;
     bench) run bench 600 python bench.py ;;
     prof) run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- \
-        python3 bench.py --no-cpu-baseline --no-host --no-c4 --no-erasure --no-latency --steps 10 ;;
+        python3 bench.py --no-cpu-baseline --no-host --no-c4 --no-latency --steps 10 ;;
     pmc)
         # one rocprofv3 pass per counter group (never combined with tracing)
         i=0
@@ -39,18 +39,19 @@ for step in "$@"; do
                 python3 tools/kernel_driver.py --reps 3
             i=$((i+1))
         done ;;
-    pmcstages)
-        # correction-kernel counters per ablation stage (tools/ablate_pmc.py, tools/pmc_stages.py)
-        i=0
-        for grp in "SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_BRANCH SQ_WAVE_CYCLES" \
-                   "SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT" \
-                   "SQ_INSTS_SMEM SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAIT_INST_LDS SQ_LDS_IDX_ACTIVE"; do
-            run pmcst$i 300 rocprofv3 --pmc $grp -d gpurun_out/pmcst$i -o pmc --output-format csv -- \
-                python3 tools/ablate_pmc.py
-            i=$((i+1))
+    traffic)
+        # HBM bytes per codeword of each bench path: FETCH_SIZE and WRITE_SIZE
+        # in separate passes per driver mode (tools/pmc_traffic.py)
+        for mode in roundtrip erasure; do
+            for c in FETCH_SIZE WRITE_SIZE; do
+                lc=$(echo $c | cut -d_ -f1 | tr A-Z a-z)
+                run traffic_${mode}_$lc 150 rocprofv3 --pmc $c -d gpurun_out/traffic/${mode}_$lc -o pmc \
+                    --output-format csv -- python3 tools/kernel_driver.py --mode $mode --reps 3
+            done
         done
-        python3 tools/pmc_stages.py gpurun_out/pmcst0 gpurun_out/pmcst1 gpurun_out/pmcst2 > gpurun_out/pmc_stages.txt 2>&1
-        cat gpurun_out/pmc_stages.txt ;;
+        python3 tools/pmc_traffic.py gpurun_out/traffic --json gpurun_out/traffic_latest.json \
+            > gpurun_out/traffic.txt 2>&1
+        cat gpurun_out/traffic.txt ;;
     *) echo "unknown step $step"; exit 2 ;;
     esac
 done

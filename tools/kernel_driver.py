@@ -1,9 +1,13 @@
 #!/usr/bin/env python3
-"""Minimal driver for profiling: REPS x (encode, inject, decode) on N codewords
-through the C ABI, nothing else (no CPU baseline, no extra passes).  Used under
-rocprofv3 by tools/gpu_session.sh (steps prof / pmc).
+"""Minimal driver for profiling: the bench's workloads through the C ABI and
+nothing else (no CPU baseline, no extra passes).  Used under rocprofv3 by
+tools/gpu_session.sh (steps prof / pmc / traffic).
 
     python tools/kernel_driver.py [--n 1048576] [--reps 5] [--mode roundtrip|erasure]
+
+As in bench.py, the encodes rotate over 3 message buffers and every decode
+works on its own corrupted copy made before the profiled loop, so no launch
+re-reads a buffer the previous launch left in the Infinity Cache.
 """
 import argparse
 import os
@@ -14,7 +18,7 @@ sys.path.insert(0, ROOT)
 
 import torch  # noqa: E402
 
-import bench
+import bench  # noqa: E402
 import devdata  # noqa: E402
 import libpoporon_amd as P  # noqa: E402
 
@@ -34,23 +38,35 @@ def main():
     ok = torch.zeros(a.n, dtype=torch.uint8, device=dev)
     cor = torch.zeros(a.n, dtype=torch.uint8, device=dev)
     s = torch.cuda.current_stream().cuda_stream
-    b = cw.data_ptr()
     if a.mode == "roundtrip":
         pos, mag = devdata.synth_errors(bench.SEED + 1, 0, a.n, 16, N, dev)
         kw = {}
+        want = 16
     else:
         pos, mag = devdata.synth_errors(bench.SEED + 2, 0, a.n, 32, K, dev)
         pos = pos.sort(dim=1).values
         slots = pos.to(torch.uint8).contiguous()
         cnt = torch.full((a.n,), 32, dtype=torch.uint8, device=dev)
         kw = dict(d_positions=slots.data_ptr(), positions_stride=32, d_counts=cnt.data_ptr())
+        want = 32
     pos8, mag8 = pos.to(torch.uint8).contiguous(), mag.to(torch.uint8).contiguous()
+    b = cw.data_ptr()
+    rs.encode_batch_device(b, N, b + K, N, K, a.n, s)
+    enc = [cw] + [cw.clone() for _ in range(2)]
+    bad = []
     for _ in range(a.reps):
-        rs.encode_batch_device(b, N, b + K, N, K, a.n, s)
-        devdata.channel(pos8, mag8, pos8.shape[1], b, N, a.n, s)
-        rs.decode_batch_device(b, N, b + K, N, K, a.n, ok.data_ptr(), cor.data_ptr(), stream=s, **kw)
+        c = cw.clone()
+        devdata.channel(pos8, mag8, pos8.shape[1], c.data_ptr(), N, a.n, s)
+        bad.append(c)
     torch.cuda.synchronize()
-    assert int(ok.sum()) == a.n, "decode failures"
+    for r in range(a.reps):
+        e = enc[r % len(enc)].data_ptr()
+        rs.encode_batch_device(e, N, e + K, N, K, a.n, s)
+        d = bad[r].data_ptr()
+        rs.decode_batch_device(d, N, d + K, N, K, a.n, ok.data_ptr(), cor.data_ptr(), stream=s, **kw)
+    torch.cuda.synchronize()
+    assert int(ok.sum()) == a.n and bool((cor == want).all()), "decode failures"
+    assert all(bool((x == cw).all()) for x in bad + enc), "decoded bytes differ"
     print("driver ok", a.mode, a.n, a.reps)
 
 
