@@ -92,7 +92,7 @@ def parse_args(argv=None):
 # ----------------------------------------------------------------------------
 # kernel ids of include/poporon_amd.h (POPORON_AMD_KERNEL_*) that make up each
 # mode's path; a path's time per step is the sum of its kernels' times
-K_ENCODE, K_REMAINDER, K_CORRECT, K_CHECK, K_BM, K_CHIEN, K_FORNEY, K_LIST, K_APPLY, K_ERASURE = range(10)
+K_ENCODE, K_REMAINDER, K_CORRECT, K_CHECK, K_BM, K_CHIEN, K_FORNEY, K_LIST, K_APPLY, K_ERASURE, K_SINGLE = range(11)
 PATHS = {
     "encode": (K_ENCODE,),
     "decode16": (K_REMAINDER, K_BM, K_CHIEN, K_FORNEY, K_APPLY, K_LIST, K_CORRECT),

@@ -131,7 +131,9 @@ bool poporon_decode_batch(poporon_t *pprn, uint8_t *data, size_t data_stride, ui
  * Omega, 5 = Chien, 6 = Forney, 8 = apply, 7 = the general kernel over the
  * codewords the split kernels hand on.  Erasure-mode batches of that size:
  * 1, 9 = the locator / Omega / Forney kernel for 32 sorted erasures (prim 1),
- * 7 = the general kernel over the rest (records), 8 = apply.
+ * 7 = the general kernel over the rest (records), 8 = apply.  A batch of
+ * one codeword (and every poporon_decode / poporon_encode call): 10 = the
+ * one-workgroup decoder (rs_dec1_k), 0 = encode (rs_enc1_k).
  *
  * Error-mode batches of at least 8192 codewords (no erasures, no external
  * syndromes) take the split decode; POPORON_AMD_DECODE_PATH=split / single
@@ -146,6 +148,7 @@ bool poporon_decode_batch(poporon_t *pprn, uint8_t *data, size_t data_stride, ui
 #define POPORON_AMD_KERNEL_LIST 7
 #define POPORON_AMD_KERNEL_APPLY 8
 #define POPORON_AMD_KERNEL_ERASURE 9
+#define POPORON_AMD_KERNEL_SINGLE 10
 bool poporon_amd_timing(poporon_t *pprn, int enable);
 bool poporon_amd_timing_read(poporon_t *pprn, int kernel, double *total_ms, uint64_t *launches);
 

@@ -17,6 +17,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
@@ -105,7 +106,7 @@ struct _poporon_config_t {
     uint8_t correction_capability; /* BCH */
 };
 
-#define NKERN 10
+#define NKERN 11
 struct TimedLaunch {
     int kernel;
     hipEvent_t a, b;
@@ -136,10 +137,11 @@ struct GpuCtx {
      * one D2H copy */
     uint8_t *stage = nullptr;
     uint8_t *hstage = nullptr;
-    /* single-call encode without copies: 256 + 32 bytes of fine-grained
-     * (coherent, GPU-uncached) host memory the kernel reads and writes
-     * directly; zc_dev is its device address, NULL if unavailable */
+    /* single-call paths without copies: ZC_BYTES of fine-grained (coherent,
+     * GPU-uncached) host memory the kernels read and write directly (layout
+     * ZC_* in rs_device.h); zc_dev is its device address, NULL if unavailable */
     uint8_t *zc = nullptr, *zc_dev = nullptr;
+    uint32_t zc_seq = 0; /* completion words of the single-call kernels */
     size_t stage_cap = 0;
     /* host-batch pipeline: PIPE_SLOTS chunks in flight, one stream each */
     struct PipeSlot {
@@ -1088,7 +1090,7 @@ static bool launch_encode(poporon_t *h, const uint8_t *d_data, size_t ds, uint8_
     if (h->fec_type == PPLN_FEC_BCH) {
         HIP_OK(bchk_encode(&h->bch, d_data, ds, d_par, ps, count, h->gpu.num_cu, s));
     } else if (h->fast && count == 1 && size <= 223) { /* one codeword: 223 dependent LFSR steps are the latency */
-        HIP_OK(rsk_encode1(h->gpu.tab, d_data, d_par, (uint32_t)size, s));
+        HIP_OK(rsk_encode1(h->gpu.tab, d_data, d_par, (uint32_t)size, nullptr, 0, s));
     } else if (h->fast) {
         HIP_OK(rsk_encode(h->gpu.tab, d_data, ds, d_par, ps, (uint32_t)size, count, h->gpu.num_cu, s));
     } else {
@@ -1107,17 +1109,13 @@ static bool launch_encode(poporon_t *h, const uint8_t *d_data, size_t ds, uint8_
 /* the split error-mode decode of one sub-batch (rs_fast.hip) */
 static bool launch_split(poporon_t *h, const RsCorrParams &prm, const RsSplitWs &ws, uint8_t *d_data, size_t ds,
                          uint8_t *d_par, size_t ps, size_t size, size_t count, uint8_t *ok, uint8_t *corrected,
-                         hipStream_t s, const uint8_t *src1)
+                         hipStream_t s)
 {
     GpuCtx &g = h->gpu;
     {
         KernelTimer t(g, POPORON_AMD_KERNEL_REMAINDER, s);
-        if (count == 1)
-            HIP_OK(rsk_syndrome1(g.tab, prm.fcr, prm.prim, src1 ? src1 : d_data, src1 ? src1 + size : d_par,
-                                 (uint32_t)size, ws.syn, ws.nlist, src1 ? d_data : nullptr, d_par, s));
-        else
-            HIP_OK(rsk_syndrome_reset(g.tab, d_data, ds, d_par, ps, (uint32_t)size, count, ws.syn, ws.nlist,
-                                      g.num_cu, s));
+        HIP_OK(rsk_syndrome_reset(g.tab, d_data, ds, d_par, ps, (uint32_t)size, count, ws.syn, ws.nlist, g.num_cu,
+                                  s));
         t.done();
     }
     {
@@ -1150,15 +1148,11 @@ static bool launch_split(poporon_t *h, const RsCorrParams &prm, const RsSplitWs 
 }
 
 /* rem / rem_cap: a workspace of rs_ws_bytes(rem_cap) bytes (rem_cap >= count)
- * owned by the caller; NULL: the handle's own.  src1 (count 1, plain decode
- * of a fast handle): the codeword's [data | parity] at a device-visible
- * address (coherent host memory), copied to d_data / d_par by the syndrome
- * kernel instead of a separate copy */
+ * owned by the caller; NULL: the handle's own */
 static bool launch_decode(poporon_t *h, uint8_t *d_data, size_t ds, uint8_t *d_par, size_t ps, size_t size,
                           size_t count, const uint16_t *ext_syn, size_t ext_stride, const uint8_t *pos8,
                           const uint32_t *pos32, size_t pos_stride, const uint8_t *cnt, uint8_t *ok,
-                          uint8_t *corrected, hipStream_t s, uint8_t *rem = nullptr, size_t rem_cap = 0,
-                          const uint8_t *src1 = nullptr)
+                          uint8_t *corrected, hipStream_t s, uint8_t *rem = nullptr, size_t rem_cap = 0)
 {
     if (h->fec_type == PPLN_FEC_BCH) {
         if (ext_syn || pos8 || pos32)
@@ -1178,11 +1172,16 @@ static bool launch_decode(poporon_t *h, uint8_t *d_data, size_t ds, uint8_t *d_p
         t.done();
         return true;
     }
-    if (src1 && (ext_syn || pos8 || pos32 || count != 1))
-        return fail("internal: a host-side source serves one plain codeword");
     RsCorrParams prm = h->corr;
     prm.size = (uint32_t)size;
     prm.pad = (int32_t)(h->rs->gf->field_size - h->rs->num_roots - size);
+    if (count == 1) { /* one codeword: one launch on one workgroup (rs_single.hip; it always runs the check) */
+        KernelTimer t(h->gpu, POPORON_AMD_KERNEL_SINGLE, s);
+        HIP_OK(rsk_decode1(h->gpu.tab, &prm, ext_syn ? 2u : (pos8 || pos32) ? 1u : 0u, d_data, d_par, pos8, pos32,
+                           cnt, 1u, ext_syn, ok, corrected, nullptr, 0, s));
+        t.done();
+        return true;
+    }
     const bool shared = !rem && !ext_syn; /* the handle's workspace */
     if (shared) {
         if (!ensure_rem(h, count) || !rem_acquire(h->gpu, s))
@@ -1198,7 +1197,7 @@ static bool launch_decode(poporon_t *h, uint8_t *d_data, size_t ds, uint8_t *d_p
         /* (sub-batches of 2^19 codewords, to keep a sub-batch's bytes in the
          * Infinity Cache until the apply, measured slower: 0.84 vs 0.75 ms
          * per bench step) */
-        if (!launch_split(h, prm, ws, d_data, ds, d_par, ps, size, count, ok, corrected, s, src1))
+        if (!launch_split(h, prm, ws, d_data, ds, d_par, ps, size, count, ok, corrected, s))
             return false;
         return !shared || rem_release(g, s);
     }
@@ -1251,11 +1250,7 @@ static bool launch_decode(poporon_t *h, uint8_t *d_data, size_t ds, uint8_t *d_p
     }
     if (!ext_syn) {
         KernelTimer t(h->gpu, POPORON_AMD_KERNEL_REMAINDER, s);
-        if (count == 1) /* one codeword: the LFSR's 255 dependent steps are the latency */
-            HIP_OK(rsk_syndrome1(h->gpu.tab, prm.fcr, prm.prim, src1 ? src1 : d_data, src1 ? src1 + size : d_par,
-                                 (uint32_t)size, rem, nullptr, src1 ? d_data : nullptr, d_par, s));
-        else
-            HIP_OK(rsk_syndrome(h->gpu.tab, d_data, ds, d_par, ps, (uint32_t)size, count, rem, h->gpu.num_cu, s));
+        HIP_OK(rsk_syndrome(h->gpu.tab, d_data, ds, d_par, ps, (uint32_t)size, count, rem, h->gpu.num_cu, s));
         t.done();
     }
     KernelTimer t(h->gpu, POPORON_AMD_KERNEL_CORRECT, s);
@@ -1772,19 +1767,53 @@ EXPORT bool poporon_decode_batch_multi_device(poporon_multi_t *m, uint8_t *const
 /* single-codeword API (the reference's entry points): a batch of one       */
 /* ------------------------------------------------------------------------ */
 
-/* the coherent host buffer of the single-call paths (GpuCtx::zc); false if
- * the device cannot address it (then the copy paths run) */
+/* the coherent host buffer of the single-call paths (GpuCtx::zc, layout
+ * ZC_* in rs_device.h); false if the device cannot address it (then the copy
+ * paths run) */
 static bool ensure_zc(GpuCtx &g)
 {
     if (!g.zc) {
         void *dp = nullptr;
-        if (hipHostMalloc((void **)&g.zc, 256 + RS_NR, hipHostMallocCoherent) == hipSuccess &&
-            hipHostGetDevicePointer(&dp, g.zc, 0) == hipSuccess)
+        if (hipHostMalloc((void **)&g.zc, ZC_BYTES, hipHostMallocCoherent) == hipSuccess &&
+            hipHostGetDevicePointer(&dp, g.zc, 0) == hipSuccess) {
             g.zc_dev = (uint8_t *)dp;
-        else
+            memset(g.zc, 0, ZC_BYTES);
+        } else {
             (void)hipGetLastError();
+        }
     }
     return g.zc_dev != nullptr;
+}
+
+/* Wait for a single-call kernel's completion word (it stores `seq` at
+ * ZC_FLAG with a system-scope release after every result): polling host
+ * memory costs the caller ~1 us after the kernel ends, a stream
+ * synchronisation several.  The stream is queried now and then so that a
+ * failed launch cannot leave the caller spinning. */
+static bool zc_wait(GpuCtx &g, uint32_t seq)
+{
+    const volatile uint32_t *f = reinterpret_cast<const volatile uint32_t *>(g.zc + ZC_FLAG);
+    for (uint32_t spin = 1;; ++spin) {
+        if (*f == seq) {
+            std::atomic_thread_fence(std::memory_order_acquire);
+            return true;
+        }
+        if ((spin & 4095u) == 0u) {
+            const hipError_t e = hipStreamQuery(g.stream);
+            if (e == hipSuccess) {
+                if (*f == seq) {
+                    std::atomic_thread_fence(std::memory_order_acquire);
+                    return true;
+                }
+                return fail("single-codeword kernel ended without its completion word");
+            }
+            if (e != hipErrorNotReady)
+                return fail("HIP error %d (%s) in a single-codeword call", (int)e, hipGetErrorString(e));
+        }
+#if defined(__x86_64__)
+        __builtin_ia32_pause();
+#endif
+    }
 }
 
 EXPORT bool poporon_encode(poporon_t *h, uint8_t *data, size_t size, uint8_t *parity)
@@ -1802,22 +1831,24 @@ EXPORT bool poporon_encode(poporon_t *h, uint8_t *data, size_t size, uint8_t *pa
     DeviceGuard dg(h->gpu.device);
     GpuCtx &g = h->gpu;
     const size_t nr = par_bytes(h);
+    /* one RS codeword: rs_enc1_k reads the message from and writes the parity
+     * to coherent host memory and signals its completion word there (one
+     * launch, no copies, no stream synchronisation) */
+    if (h->fec_type == PPLN_FEC_RS && h->fast && size >= 1 && size <= 223 && ensure_zc(g)) {
+        memcpy(g.zc + ZC_DATA, data, size);
+        const uint32_t seq = ++g.zc_seq;
+        KernelTimer t(g, POPORON_AMD_KERNEL_ENCODE, g.stream);
+        HIP_OK(rsk_encode1(g.tab, g.zc_dev + ZC_DATA, g.zc_dev + ZC_PAR, (uint32_t)size,
+                           reinterpret_cast<uint32_t *>(g.zc_dev + ZC_FLAG), seq, g.stream));
+        t.done();
+        if (!zc_wait(g, seq))
+            return false;
+        memcpy(parity, g.zc + ZC_PAR, nr);
+        return true;
+    }
     const size_t off_p = (size + 15) & ~(size_t)15;
     if (!ensure_stage(h, off_p + nr + 16))
         return false;
-    /* one RS codeword: rs_enc1_k reads the message from and writes the
-     * parity to coherent host memory, no copies (a launch and a sync) */
-    if (h->fec_type == PPLN_FEC_RS && h->fast && size >= 1 && size <= 223) {
-        if (ensure_zc(g)) {
-            memcpy(g.zc, data, size);
-            KernelTimer t(g, POPORON_AMD_KERNEL_ENCODE, g.stream);
-            HIP_OK(rsk_encode1(g.tab, g.zc_dev, g.zc_dev + 256, (uint32_t)size, g.stream));
-            t.done();
-            HIP_OK(hipStreamSynchronize(g.stream));
-            memcpy(parity, g.zc + 256, nr);
-            return true;
-        }
-    }
     /* pinned mirror: one H2D copy in, one D2H copy out */
     if (size) {
         memcpy(g.hstage, data, size);
@@ -1874,13 +1905,7 @@ EXPORT bool poporon_decode(poporon_t *h, uint8_t *data, size_t size, uint8_t *pa
         return false;
     size_t fixed = 0;
     bool success = false;
-    if (!check_decode_size(h, size)) {
-        h->last_corrected = 0;
-        if (corrected_num)
-            *corrected_num = 0;
-        return false;
-    }
-    if (!gpu_init(h)) {
+    if (!check_decode_size(h, size) || !gpu_init(h)) {
         h->last_corrected = 0;
         if (corrected_num)
             *corrected_num = 0;
@@ -1890,63 +1915,95 @@ EXPORT bool poporon_decode(poporon_t *h, uint8_t *data, size_t size, uint8_t *pa
         DeviceGuard dg(h->gpu.device);
         GpuCtx &g = h->gpu;
         const size_t nr = h->rs->num_roots;
-        /* stage layout: [data | parity | ok | cor | pad | syndromes (nr x u16) or slots (nr x u32) | count] */
-        const size_t off_p = size, off_ok = size + nr, off_cor = off_ok + 1;
-        const size_t off_x = (off_cor + 1 + 15) & ~(size_t)15;
-        if (!ensure_stage(h, off_x + nr * 4 + 16))
-            return false;
-        /* everything goes through the pinned mirror: one H2D copy of
-         * [data | parity | ok | cor | pad | syndromes or slots + count], the
-         * kernels, one D2H copy of [data | parity | ok | cor] */
-        uint8_t *hs = g.hstage;
-        const uint16_t *ext = nullptr;
-        const uint32_t *pos32 = nullptr;
-        const uint8_t *cnt = nullptr;
-        bool refuse = false;
-        size_t in_bytes = off_cor + 1;
-        memcpy(hs, data, size);
-        memcpy(hs + off_p, parity, nr);
-        if (h->ext_syndrome) {
-            for (size_t i = 0; i < nr; i++)
-                refuse |= h->ext_syndrome[i] > h->rs->gf->field_size; /* out-of-table index in the reference */
-            memcpy(hs + off_x, h->ext_syndrome, nr * sizeof(uint16_t));
-            in_bytes = off_x + nr * sizeof(uint16_t);
-            ext = (const uint16_t *)(g.stage + off_x);
-        } else if (h->erasure) {
-            const poporon_erasure_t *e = h->erasure;
-            /* the reference reads slots by root ordinal (quirks Q2/Q3): copy nr
-             * slots, those past the list's capacity read as 0 */
-            memset(hs + off_x, 0, nr * 4);
-            memcpy(hs + off_x, e->erasure_positions, std::min<size_t>(e->capacity, nr) * sizeof(uint32_t));
-            /* counts past num_roots (quirk Q5) reach the kernel as they are
-             * (clamped to 255): refused there only for a dirty codeword */
-            hs[off_x + nr * 4] = (uint8_t)std::min<uint32_t>(e->erasure_count, 255u);
-            in_bytes = off_x + nr * 4 + 1;
-            pos32 = (const uint32_t *)(g.stage + off_x);
-            cnt = g.stage + off_x + nr * 4;
-        }
-        /* plain decode of a fast handle: the syndrome kernel reads the
-         * codeword from coherent host memory and copies it to the stage (one
-         * copy fewer on the critical path) */
-        const bool zc = !ext && !pos32 && h->fast && ensure_zc(g);
-        if (refuse) {
-            fail("external syndrome > field size: undefined in the reference, refused");
+        if (h->fast && ensure_zc(g)) {
+            /* rs_dec1_k: the whole decode of one codeword in one launch, reading
+             * the codeword, the erasure slots or the external syndromes from
+             * coherent host memory and writing back the corrected bytes, ok and
+             * corrected_num, then its completion word */
+            uint8_t *z = g.zc;
+            memcpy(z + ZC_DATA, data, size);
+            memcpy(z + ZC_PAR, parity, nr);
+            uint32_t mode = 0;
+            if (h->ext_syndrome) {
+                mode = 2; /* values > 255 are refused by the kernel (out-of-table in the reference) */
+                memcpy(z + ZC_EXT, h->ext_syndrome, nr * sizeof(uint16_t));
+            } else if (h->erasure) {
+                mode = 1;
+                const poporon_erasure_t *e = h->erasure;
+                /* the reference reads slots by root ordinal (quirks Q2/Q3): nr
+                 * slots, those past the list's capacity read as 0; the count as
+                 * it is (past num_roots: refused for a dirty codeword, Q5) */
+                uint32_t *pos = reinterpret_cast<uint32_t *>(z + ZC_POS);
+                const size_t have = std::min<size_t>(e->capacity, nr);
+                memcpy(pos, e->erasure_positions, have * sizeof(uint32_t));
+                memset(pos + have, 0, (nr - have) * sizeof(uint32_t));
+                *reinterpret_cast<uint32_t *>(z + ZC_CNT) = e->erasure_count;
+            }
+            RsCorrParams prm = h->corr;
+            prm.size = (uint32_t)size;
+            prm.pad = (int32_t)(h->rs->gf->field_size - h->rs->num_roots - size);
+            uint8_t *zd = g.zc_dev;
+            const uint32_t seq = ++g.zc_seq;
+            KernelTimer t(g, POPORON_AMD_KERNEL_SINGLE, g.stream);
+            HIP_OK(rsk_decode1(g.tab, &prm, mode, zd + ZC_DATA, zd + ZC_PAR, nullptr,
+                               reinterpret_cast<const uint32_t *>(zd + ZC_POS), zd + ZC_CNT, 4u,
+                               reinterpret_cast<const uint16_t *>(zd + ZC_EXT), zd + ZC_OK, zd + ZC_COR,
+                               reinterpret_cast<uint32_t *>(zd + ZC_FLAG), seq, g.stream));
+            t.done();
+            if (!zc_wait(g, seq))
+                return false;
+            memcpy(data, z + ZC_DATA, size);
+            memcpy(parity, z + ZC_PAR, nr);
+            success = z[ZC_OK] != 0;
+            fixed = z[ZC_COR];
         } else {
-            if (zc) {
-                memcpy(g.zc, data, size);
-                memcpy(g.zc + size, parity, nr);
+            /* general parameters (rs_generic.hip): everything through the pinned
+             * mirror, one H2D copy of [data | parity | ok | cor | pad | syndromes
+             * (nr x u16) or slots (nr x u32) + count], the kernel, one D2H copy of
+             * [data | parity | ok | cor] */
+            const size_t off_p = size, off_ok = size + nr, off_cor = off_ok + 1;
+            const size_t off_x = (off_cor + 1 + 15) & ~(size_t)15;
+            if (!ensure_stage(h, off_x + nr * 4 + 16))
+                return false;
+            uint8_t *hs = g.hstage;
+            const uint16_t *ext = nullptr;
+            const uint32_t *pos32 = nullptr;
+            const uint8_t *cnt = nullptr;
+            bool refuse = false;
+            size_t in_bytes = off_cor + 1;
+            memcpy(hs, data, size);
+            memcpy(hs + off_p, parity, nr);
+            if (h->ext_syndrome) {
+                for (size_t i = 0; i < nr; i++)
+                    refuse |= h->ext_syndrome[i] > h->rs->gf->field_size; /* out-of-table index in the reference */
+                memcpy(hs + off_x, h->ext_syndrome, nr * sizeof(uint16_t));
+                in_bytes = off_x + nr * sizeof(uint16_t);
+                ext = (const uint16_t *)(g.stage + off_x);
+            } else if (h->erasure) {
+                const poporon_erasure_t *e = h->erasure;
+                memset(hs + off_x, 0, nr * 4);
+                memcpy(hs + off_x, e->erasure_positions, std::min<size_t>(e->capacity, nr) * sizeof(uint32_t));
+                /* counts past num_roots (quirk Q5) reach the kernel clamped to 255:
+                 * refused there only for a dirty codeword */
+                hs[off_x + nr * 4] = (uint8_t)std::min<uint32_t>(e->erasure_count, 255u);
+                in_bytes = off_x + nr * 4 + 1;
+                pos32 = (const uint32_t *)(g.stage + off_x);
+                cnt = g.stage + off_x + nr * 4;
+            }
+            if (refuse) {
+                fail("external syndrome > field size: undefined in the reference, refused");
             } else {
                 HIP_OK(hipMemcpyAsync(g.stage, hs, in_bytes, hipMemcpyHostToDevice, g.stream));
+                if (!launch_decode(h, g.stage, size, g.stage + off_p, nr, size, 1, ext, nr, nullptr, pos32, nr, cnt,
+                                   g.stage + off_ok, g.stage + off_cor, g.stream))
+                    return false;
+                HIP_OK(hipMemcpyAsync(hs, g.stage, off_cor + 1, hipMemcpyDeviceToHost, g.stream));
+                HIP_OK(hipStreamSynchronize(g.stream));
+                memcpy(data, hs, size);
+                memcpy(parity, hs + off_p, nr);
+                success = hs[off_ok] != 0;
+                fixed = hs[off_cor];
             }
-            if (!launch_decode(h, g.stage, size, g.stage + off_p, nr, size, 1, ext, nr, nullptr, pos32, nr, cnt,
-                               g.stage + off_ok, g.stage + off_cor, g.stream, nullptr, 0, zc ? g.zc_dev : nullptr))
-                return false;
-            HIP_OK(hipMemcpyAsync(hs, g.stage, off_cor + 1, hipMemcpyDeviceToHost, g.stream));
-            HIP_OK(hipStreamSynchronize(g.stream));
-            memcpy(data, hs, size);
-            memcpy(parity, hs + off_p, nr);
-            success = hs[off_ok] != 0;
-            fixed = hs[off_cor];
         }
     }
     h->last_corrected = fixed;

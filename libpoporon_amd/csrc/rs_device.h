@@ -136,17 +136,31 @@ hipError_t rsk_syndrome_reset(const RsDevTables *tab, const uint8_t *data, size_
                               size_t pstride, uint32_t size, size_t count, uint8_t *syn, uint32_t *reset, int num_cu,
                               hipStream_t stream);
 
-/* parity of one codeword of size <= 223 as the sum of the table rows encq
- * (one workgroup): the single-call encode; same bytes as rsk_encode */
-hipError_t rsk_encode1(const RsDevTables *tab, const uint8_t *data, uint8_t *parity, uint32_t size,
-                       hipStream_t stream);
+/* One codeword per launch on one workgroup (rs_single.hip): the single-call
+ * paths and batches of one.  flag (may be NULL): `seq` is stored there with
+ * a system-scope release after every result (the host polls it).
+ *   rsk_encode1  parity of a message of size <= 223
+ *   rsk_decode1  rs_decode for one codeword: mode 0 plain, 1 erasure (pos8 or
+ *                pos32 slots, count of cnt_bytes = 1 or 4 bytes at cnt), 2
+ *                external log-form syndromes (ext, 32 x u16); ok / corrected
+ *                one byte each */
+hipError_t rsk_encode1(const RsDevTables *tab, const uint8_t *data, uint8_t *parity, uint32_t size, uint32_t *flag,
+                       uint32_t seq, hipStream_t stream);
+hipError_t rsk_decode1(const RsDevTables *tab, const RsCorrParams *prm, uint32_t mode, uint8_t *data,
+                       uint8_t *parity, const uint8_t *pos8, const uint32_t *pos32, const void *cnt,
+                       uint32_t cnt_bytes, const uint16_t *ext, uint8_t *ok, uint8_t *corrected, uint32_t *flag,
+                       uint32_t seq, hipStream_t stream);
 
-/* the same for one codeword (data, parity: its bytes), by direct evaluation
- * on one workgroup: the single-call latency path; reset as above (may be
- * NULL); dst_data / dst_parity (may be NULL): copy the codeword there */
-hipError_t rsk_syndrome1(const RsDevTables *tab, uint32_t fcr, uint32_t prim, const uint8_t *data,
-                         const uint8_t *parity, uint32_t size, uint8_t *syn, uint32_t *reset, uint8_t *dst_data,
-                         uint8_t *dst_parity, hipStream_t stream);
+/* layout of the coherent host buffer of the single-call API (GpuCtx::zc) */
+#define ZC_DATA 0    /* message / data bytes (<= 223) */
+#define ZC_PAR 256   /* 32 parity bytes */
+#define ZC_POS 320   /* 32 erasure slots, u32 */
+#define ZC_CNT 448   /* erasure count, u32 */
+#define ZC_EXT 512   /* 32 external syndromes, u16 */
+#define ZC_OK 576
+#define ZC_COR 577
+#define ZC_FLAG 640  /* u32 completion word */
+#define ZC_BYTES 1024
 
 /* poly syndromes (32 B per codeword, rsk_syndrome) -> log form: out[c*stride + i]
  * = log S_i (255 = zero), flag[c] = any S_i nonzero; out / flag may be NULL */

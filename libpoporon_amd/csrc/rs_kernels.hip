@@ -544,113 +544,6 @@ extern "C" hipError_t rsk_syndrome_reset(const RsDevTables *tab, const uint8_t *
     return launch_lfsr<MODE_SYNDROME>(tab, data, dstride, parity, pstride, size, count, syn, num_cu, stream, reset);
 }
 
-/* One codeword's parity (the single-call encode, size <= 223): the LFSR of
- * src/encode.c:120-143 is GF-linear in the message, so parity byte m is
- * sum_j data_j Q[size-1-j]_m with Q[d] the parity of a one-byte message 1
- * followed by d zeros (RsDevTables::encq, log form, built on the host by
- * running that LFSR).  Thread t: byte t & 31 over j = t >> 5 (mod 8); the
- * eight partial sums are XORed in LDS. */
-__global__ __launch_bounds__(256) void rs_enc1_k(const RsDevTables *__restrict__ T, const uint8_t *__restrict__ data,
-                                                 uint8_t *__restrict__ parity, uint32_t size)
-{
-    __shared__ uint8_t ex[512];
-    __shared__ uint8_t lg[256];
-    __shared__ uint8_t msg[256];
-    __shared__ uint32_t part[256];
-    const uint32_t t = threadIdx.x;
-    ex[t] = T->exp2[t];
-    ex[t + 256] = T->exp2[t + 256];
-    lg[t] = T->log[t];
-    if (t < size) /* one load per byte, all in flight together (data may be host memory) */
-        msg[t] = data[t];
-    __syncthreads();
-    const uint32_t m = t & 31u;
-    uint32_t acc = 0;
-    for (uint32_t j = t >> 5; j < size; j += 8) {
-        const uint32_t v = msg[j], q = T->encq[(size - 1u - j) * RS_NR + m];
-        if (v && q != 255u)
-            acc ^= ex[lg[v] + q];
-    }
-    part[t] = acc;
-    __syncthreads();
-    if (t < RS_NR) {
-        uint32_t v = 0;
-#pragma unroll
-        for (int k = 0; k < 8; ++k)
-            v ^= part[t + 32u * k];
-        parity[t] = (uint8_t)v;
-    }
-}
-
-extern "C" hipError_t rsk_encode1(const RsDevTables *tab, const uint8_t *data, uint8_t *parity, uint32_t size,
-                                  hipStream_t stream)
-{
-    hipLaunchKernelGGL(rs_enc1_k, dim3(1), dim3(256), 0, stream, tab, data, parity, size);
-    return hipGetLastError();
-}
-
-/* One codeword's syndromes by direct evaluation (the single-call path, where
- * the LFSR's 255 dependent steps on one lane are the latency): S_i =
- * sum_j w_j beta_i^(L-1-j), w = data || parity, L = size + 32, beta_i =
- * alpha^(prim (fcr + i)) -- the field elements of src/decode.c:375-415 and of
- * the remainder kernel.  The codeword is staged in LDS with one load per
- * byte (the source may be host memory; with dst_data the bytes are also
- * copied there, for the correction kernel).  Thread t: syndrome t & 31 over
- * bytes j = t >> 5 (mod 8); the eight partial sums are XORed in LDS. */
-__global__ __launch_bounds__(256) void rs_syn1_k(const RsDevTables *__restrict__ T, uint32_t fcr, uint32_t prim,
-                                                 const uint8_t *data, const uint8_t *parity, uint32_t size,
-                                                 uint8_t *__restrict__ syn, uint32_t *__restrict__ reset,
-                                                 uint8_t *dst_data, uint8_t *dst_parity)
-{
-    __shared__ uint8_t ex[512];
-    __shared__ uint8_t lg[256];
-    __shared__ uint8_t w[256];
-    __shared__ uint32_t part[256];
-    const uint32_t t = threadIdx.x, L = size + RS_NR;
-    ex[t] = T->exp2[t];
-    ex[t + 256] = T->exp2[t + 256];
-    lg[t] = T->log[t];
-    if (t < L) {
-        const uint8_t v = t < size ? data[t] : parity[t - size];
-        w[t] = v;
-        if (dst_data) {
-            if (t < size)
-                dst_data[t] = v;
-            else
-                dst_parity[t - size] = v;
-        }
-    }
-    if (reset && t == 0)
-        *reset = 0;
-    __syncthreads();
-    const uint32_t i = t & 31u;
-    const uint32_t b = (prim * (fcr + i)) % 255u;
-    uint32_t acc = 0;
-    for (uint32_t j = t >> 5; j < L; j += 8) {
-        const uint32_t v = w[j];
-        if (v)
-            acc ^= ex[lg[v] + (b * (L - 1u - j)) % 255u];
-    }
-    part[t] = acc;
-    __syncthreads();
-    if (t < RS_NR) {
-        uint32_t v = 0;
-#pragma unroll
-        for (int k = 0; k < 8; ++k)
-            v ^= part[t + 32u * k];
-        syn[t] = (uint8_t)v;
-    }
-}
-
-extern "C" hipError_t rsk_syndrome1(const RsDevTables *tab, uint32_t fcr, uint32_t prim, const uint8_t *data,
-                                    const uint8_t *parity, uint32_t size, uint8_t *syn, uint32_t *reset,
-                                    uint8_t *dst_data, uint8_t *dst_parity, hipStream_t stream)
-{
-    hipLaunchKernelGGL(rs_syn1_k, dim3(1), dim3(256), 0, stream, tab, fcr, prim, data, parity, size, syn, reset,
-                       dst_data, dst_parity);
-    return hipGetLastError();
-}
-
 /* poly-form syndromes (rsk_syndrome's output) -> the reference's log form:
  * uint16 log S_i (255 = zero) and the "any nonzero" flag (src/decode.c:409-414) */
 __global__ __launch_bounds__(256) void rs_synlog_k(const RsDevTables *__restrict__ T, const uint8_t *__restrict__ syn,
