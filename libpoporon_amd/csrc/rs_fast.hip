@@ -57,6 +57,7 @@
 #define SZ (128u * Z0 - 1u)
 #define FORNEY_R 1     /* roots per Forney step (more spill at 64 VGPRs) */
 #define FORNEY_WAVES 8
+#define BWG 1024 /* rs_bm_k: 8 waves/SIMD; 4 or 6 measured slower (profiles/r03_bm_experiments.log) */
 #define BM_WAVES 8
 
 /* ------------------------------------------------------------------------ */
@@ -65,16 +66,22 @@
 
 /* the table image (RsDevTables::gfa) into LDS: every load first, then the
  * stores (a rolled copy waits for each load: one L2 round trip apiece) */
+template <int WG = FWG>
 __device__ __forceinline__ void fill_gfa(uint32_t *lgf, const RsDevTables *__restrict__ T)
 {
-    constexpr int K = 512 * 32 / 4 / FWG;
+    if constexpr ((512 * 32 / 4) % WG != 0) {
+        for (uint32_t t = threadIdx.x; t < 512u * 32u / 4u; t += WG)
+            reinterpret_cast<uint4 *>(lgf)[t] = T->gfa[t];
+        return;
+    }
+    constexpr int K = 512 * 32 / 4 / WG;
     uint4 v[K];
 #pragma unroll
     for (int k = 0; k < K; ++k)
-        v[k] = T->gfa[threadIdx.x + k * FWG];
+        v[k] = T->gfa[threadIdx.x + k * WG];
 #pragma unroll
     for (int k = 0; k < K; ++k)
-        reinterpret_cast<uint4 *>(lgf)[threadIdx.x + k * FWG] = v[k];
+        reinterpret_cast<uint4 *>(lgf)[threadIdx.x + k * WG] = v[k];
 }
 
 struct GfA {
@@ -129,21 +136,21 @@ static int fast_grid(size_t count, int num_cu)
  * i of iteration r = 4q+1+s reads entry 3 - s + i at a compile-time place
  * (the four iterations are unrolled; blocks are a rolled loop).
  */
-__global__ __launch_bounds__(FWG, BM_WAVES) void rs_bm_k(const RsDevTables *__restrict__ T, const uint8_t *__restrict__ syn,
+__global__ __launch_bounds__(BWG, BM_WAVES) void rs_bm_k(const RsDevTables *__restrict__ T, const uint8_t *__restrict__ syn,
                                                    size_t count, uint8_t *__restrict__ lamo, uint8_t *__restrict__ omo,
                                                    uint8_t *__restrict__ meta, uint32_t *__restrict__ list,
                                                    uint32_t *__restrict__ nlist, uint8_t *__restrict__ ok,
                                                    uint8_t *__restrict__ corrected)
 {
     __shared__ uint32_t lgf[512 * 32];
-    fill_gfa(lgf, T);
+    fill_gfa<BWG>(lgf, T);
     __syncthreads();
     const GfA gf{lds_addr(lgf) + 4u * (threadIdx.x & 31u) + 1u};
     const uint32_t pofs = gf.pofs;
     const uint32_t AZ = gf.az();         /* address-form zero */
     constexpr uint32_t DQZ = SZ;         /* "no update": dq + B's logs read zeros */
 
-    for (size_t base = (size_t)blockIdx.x * FWG; base < count; base += (size_t)gridDim.x * FWG) {
+    for (size_t base = (size_t)blockIdx.x * BWG; base < count; base += (size_t)gridDim.x * BWG) {
         const size_t cw = base + threadIdx.x;
         const bool valid = cw < count;
         const uint32_t *sp = reinterpret_cast<const uint32_t *>(syn + (valid ? cw : 0) * RS_NR);
@@ -978,7 +985,9 @@ extern "C" hipError_t rsk_bm(const RsDevTables *tab, const RsSplitWs *ws, size_t
 {
     if (count == 0)
         return hipSuccess;
-    hipLaunchKernelGGL(rs_bm_k, dim3(fast_grid(count, num_cu)), dim3(FWG), 0, stream, tab, ws->syn, count, ws->lam,
+    const size_t need = (count + BWG - 1) / BWG, res = (size_t)(num_cu > 0 ? num_cu : 256) * (BM_WAVES * 256 / BWG);
+    hipLaunchKernelGGL(rs_bm_k, dim3((uint32_t)(need < res ? need : res)), dim3(BWG), 0, stream, tab, ws->syn, count,
+                       ws->lam,
                        ws->om, ws->meta, ws->list, ws->nlist, ok, corrected);
     return hipGetLastError();
 }
