@@ -49,68 +49,15 @@
 #include <type_traits>
 
 #include "rs_device.h"
+#include "rs_gfa.h"
 #include "rs_lane.h"
 
 #define FWG 1024       /* threads per workgroup; two workgroups per CU */
 #define NL 17          /* Lambda_0..16 and B_0..16: t = 16 */
-#define Z0 RS_Z0       /* zero sentinels: AZ = 128 Z0 + 4r, SZ = 128 Z0 - 1 (see the header) */
-#define SZ (128u * Z0 - 1u)
 #define FORNEY_R 1     /* roots per Forney step (more spill at 64 VGPRs) */
 #define FORNEY_WAVES 8
 #define BWG 1024 /* rs_bm_k: 8 waves/SIMD; 4 or 6 measured slower (profiles/r03_bm_experiments.log) */
 #define BM_WAVES 8
-
-/* ------------------------------------------------------------------------ */
-/* GF table (rs_bm_k, rs_forney_k)                                          */
-/* ------------------------------------------------------------------------ */
-
-/* the table image (RsDevTables::gfa) into LDS: every load first, then the
- * stores (a rolled copy waits for each load: one L2 round trip apiece) */
-template <int WG = FWG>
-__device__ __forceinline__ void fill_gfa(uint32_t *lgf, const RsDevTables *__restrict__ T)
-{
-    if constexpr ((512 * 32 / 4) % WG != 0) {
-        for (uint32_t t = threadIdx.x; t < 512u * 32u / 4u; t += WG)
-            reinterpret_cast<uint4 *>(lgf)[t] = T->gfa[t];
-        return;
-    }
-    constexpr int K = 512 * 32 / 4 / WG;
-    uint4 v[K];
-#pragma unroll
-    for (int k = 0; k < K; ++k)
-        v[k] = T->gfa[threadIdx.x + k * WG];
-#pragma unroll
-    for (int k = 0; k < K; ++k)
-        reinterpret_cast<uint4 *>(lgf)[threadIdx.x + k * WG] = v[k];
-}
-
-struct GfA {
-    uint32_t pofs; /* 4 (lane & 31) + 1: this replica's exp byte of log 0 */
-    /* this replica's address-form zero */
-    __device__ __forceinline__ uint32_t az() const { return pofs + SZ; }
-    /* exp of an address-form log plus a plain scaled log */
-    __device__ __forceinline__ uint32_t expa(uint32_t a) const { return lds8(a); }
-    /* address-form log of v < 256 (AZ for 0) */
-    __device__ __forceinline__ uint32_t loga(uint32_t v) const { return lds16(pofs + 1u + (v << 7)); }
-    /* plain scaled log 128 log v (SZ for 0) */
-    __device__ __forceinline__ uint32_t logs(uint32_t v) const { return loga(v) - pofs; }
-    /* log (0..254) of an address-form log, 255 for zero */
-    __device__ __forceinline__ uint32_t plog(uint32_t a) const { return (a & 1u) ? (a - pofs) >> 7 : 255u; }
-    /* address-form log of a stored byte log (255 = zero) */
-    __device__ __forceinline__ uint32_t afrom(uint32_t b) const { return b < 255u ? (b << 7) + pofs : az(); }
-    /* alpha^l of a plain log l < 255 */
-    __device__ __forceinline__ uint32_t exp(uint32_t l) const { return lds8(pofs + (l << 7)); }
-};
-
-/* compile-time loop: f(std::integral_constant<int, i>) for i = I, I+S, ... < E */
-template <int I, int E, int S, class F>
-__device__ __forceinline__ void static_for(F &&f)
-{
-    if constexpr (I < E) {
-        f(std::integral_constant<int, I>{});
-        static_for<I + S, E, S>(f);
-    }
-}
 
 static int fast_grid(size_t count, int num_cu)
 {
@@ -498,7 +445,7 @@ __global__ __launch_bounds__(FWG, FORNEY_WAVES) void rs_forney_k(const RsDevTabl
                                                        uint8_t *__restrict__ corrected)
 {
     __shared__ uint32_t lgf[512 * 32];
-    fill_gfa(lgf, T);
+    fill_gfa<FWG>(lgf, T);
     __syncthreads();
     const GfA gf{lds_addr(lgf) + 4u * (threadIdx.x & 31u) + 1u};
     const int32_t pad = P.pad;
@@ -641,15 +588,20 @@ __global__ __launch_bounds__(FWG, FORNEY_WAVES) void rs_forney_k(const RsDevTabl
  * list (rs_correct_k in record mode).  Output: the 64-byte record of
  * rs_apply_k<32> (slots, magnitudes).
  *
- * Registers (64 at 8 waves/SIMD): the locator in 31 address-form logs, then
- * packed two per register for Omega (16 + 16 syndrome logs + 16 Omega) and
- * Forney (Omega, odd Lambda: 24); slots are re-read where needed.
+ * Registers: the locator in 31 address-form logs, then packed two per
+ * register for Omega (16 + 16 syndrome logs + 16 Omega); Forney reads Omega
+ * and the odd Lambda terms unpacked (48 registers, 4 waves/SIMD: the kernel
+ * is issue-bound, occupancy 4, 6 and 8 measured the same) and splits each
+ * sum at m = 16, so one 16-step power chain per root serves both halves
+ * (0.36 -> 0.31-0.33 ms, profiles/r03_era_experiments.log); slots are
+ * re-read where needed.
  */
-#define ERA_WAVES 6 /* 80 VGPRs: 0.351 ms per 2^20 codewords; 4: 0.358, 8 (a few spills outside the loops): 0.365 */
+#define EWG 1024 /* rs_era_k: 4 waves/SIMD; 6 (768-thread groups) and 8 measured the same: issue-bound (profiles/r03_era_experiments.log) */
+#define ERA_WAVES 4
 #define ERA_R 4 /* Forney roots per step: one record dword */
 #define ERA_OG 8 /* Omega lookups per group */
 
-__global__ __launch_bounds__(FWG, ERA_WAVES) void rs_era_k(const RsDevTables *__restrict__ T, RsCorrParams P,
+__global__ __launch_bounds__(EWG, ERA_WAVES) void rs_era_k(const RsDevTables *__restrict__ T, RsCorrParams P,
                                                          const uint8_t *__restrict__ syn,
                                                          const uint8_t *__restrict__ pos8, size_t pos_stride,
                                                          const uint8_t *__restrict__ cntp, size_t count,
@@ -658,7 +610,7 @@ __global__ __launch_bounds__(FWG, ERA_WAVES) void rs_era_k(const RsDevTables *__
                                                          uint8_t *__restrict__ ok, uint8_t *__restrict__ corrected)
 {
     __shared__ uint32_t lgf[512 * 32];
-    fill_gfa(lgf, T);
+    fill_gfa<EWG>(lgf, T);
     __syncthreads();
     const GfA gf{lds_addr(lgf) + 4u * (threadIdx.x & 31u) + 1u};
     const uint32_t pofs = gf.pofs;
@@ -668,7 +620,7 @@ __global__ __launch_bounds__(FWG, ERA_WAVES) void rs_era_k(const RsDevTables *__
     auto red7 = [](uint32_t x) __attribute__((always_inline)) { return min(x, x - M255); };
     const uint32_t lim = P.size + RS_NR, pad = (uint32_t)P.pad;
 
-    for (size_t base = (size_t)blockIdx.x * FWG; base < count; base += (size_t)gridDim.x * FWG) {
+    for (size_t base = (size_t)blockIdx.x * EWG; base < count; base += (size_t)gridDim.x * EWG) {
         const size_t cw = base + threadIdx.x;
         const bool valid = cw < count;
         uint4 sa = make_uint4(0, 0, 0, 0), sb = sa, pa = sa, pb = sa;
@@ -823,53 +775,73 @@ __global__ __launch_bounds__(FWG, ERA_WAVES) void rs_era_k(const RsDevTables *__
          * a zero numerator corrects nothing and is not counted ---- */
         uint32_t ncor = 0;
         const uint32_t *slw = reinterpret_cast<const uint32_t *>(slots);
+        uint32_t opu[RS_NR], alou[RS_NR / 2]; /* unpacked once: plain adds in the loop, not SDWA word selects */
+#pragma unroll
+        for (int m = 0; m < RS_NR; ++m)
+            opu[m] = half(op, m);
+#pragma unroll
+        for (int h = 0; h < RS_NR / 2; ++h)
+            alou[h] = half(alo, h);
 #pragma unroll 1
         for (uint32_t q = 0; q < RS_NR / ERA_R; ++q) {
-            const uint32_t w = fast ? slw[q] : 0u;
-            /* opaque per step: the halves are unpacked at their use, not
-             * hoisted out of the loop (48 registers) */
+            uint32_t w[ERA_R / 4];
 #pragma unroll
-            for (int k = 0; k < RS_NR / 2; ++k)
-                asm volatile("" : "+v"(op[k]));
-#pragma unroll
-            for (int k = 0; k < RS_NR / 4; ++k)
-                asm volatile("" : "+v"(alo[k]));
+            for (int k = 0; k < ERA_R / 4; ++k)
+                w[k] = fast ? slw[q * (ERA_R / 4) + k] : 0u;
             uint32_t ii[ERA_R], si[ERA_R], s[ERA_R], num[ERA_R], den[ERA_R];
 #pragma unroll
             for (int t = 0; t < ERA_R; ++t) {
-                ii[t] = ((w >> (8 * t)) & 0xffu) + pad + 1u; /* the Chien point, 1..255 */
+                ii[t] = ((w[t >> 2] >> (8 * (t & 3))) & 0xffu) + pad + 1u; /* the Chien point, 1..255 */
                 si[t] = 128u * (ii[t] == 255u ? 0u : ii[t]);
                 s[t] = 0;
                 num[t] = 0;
                 den[t] = 0;
             }
+            /* m = 16 a + b: num = N_0 + alpha^(16 i) N_1, N_a = sum_b Omega_(16a+b)
+             * alpha^(b i), and den likewise over the even b: one power chain
+             * of 16 steps per root instead of 32 */
+            uint32_t nh[ERA_R], dh[ERA_R];
 #pragma unroll
-            for (int m = 0; m < RS_NR; ++m) {
+            for (int t = 0; t < ERA_R; ++t)
+                nh[t] = dh[t] = 0;
+#pragma unroll
+            for (int b = 0; b < RS_NR / 2; ++b) {
 #pragma unroll
                 for (int t = 0; t < ERA_R; ++t) {
-                    num[t] ^= gf.expa(half(op, m) + s[t]);
-                    if ((m & 1) == 0)
-                        den[t] ^= gf.expa(half(alo, m >> 1) + s[t]);
+                    num[t] ^= gf.expa(opu[b] + s[t]);
+                    nh[t] ^= gf.expa(opu[b + 16] + s[t]);
+                    if ((b & 1) == 0) {
+                        den[t] ^= gf.expa(alou[b >> 1] + s[t]);
+                        dh[t] ^= gf.expa(alou[(b >> 1) + 8] + s[t]);
+                    }
                     s[t] = addmod7(s[t], si[t]);
                 }
-                if (m & 1) {
+                if (b & 1) {
 #pragma unroll
                     for (int t = 0; t < ERA_R; ++t)
-                        asm volatile("" : "+v"(num[t]), "+v"(den[t]));
+                        asm volatile("" : "+v"(num[t]), "+v"(den[t]), "+v"(nh[t]), "+v"(dh[t]));
                     __builtin_amdgcn_sched_barrier(0); /* two powers at a time: registers */
                 }
             }
-            uint32_t cur = 0;
+#pragma unroll
+            for (int t = 0; t < ERA_R; ++t) { /* s = 128 (16 i mod 255) */
+                num[t] ^= gf.expa(gf.loga(nh[t]) + s[t]);
+                den[t] ^= gf.expa(gf.loga(dh[t]) + s[t]);
+            }
+            uint32_t cur[ERA_R / 4] = {};
 #pragma unroll
             for (int t = 0; t < ERA_R; ++t) {
                 const uint32_t ln2 = mod255((uint32_t)((int32_t)ii[t] * ((int32_t)P.fcr - 1) + (int32_t)RS_NN));
                 const uint32_t lnum = gf.plog(gf.loga(num[t])), lden = gf.plog(gf.loga(den[t]));
                 const bool z = num[t] != 0u;
                 ncor += z ? 1u : 0u;
-                cur |= (z ? gf.exp((lnum + ln2 + RS_NN - lden) % 255u) : 0u) << (8 * t);
+                cur[t >> 2] |= (z ? gf.exp((lnum + ln2 + RS_NN - lden) % 255u) : 0u) << (8 * (t & 3));
             }
-            if (fast)
-                recw[8 + q] = cur;
+            if (fast) {
+#pragma unroll
+                for (int k = 0; k < ERA_R / 4; ++k)
+                    recw[8 + q * (ERA_R / 4) + k] = cur[k];
+            }
         }
         if (fast) {
             meta[cw] = (uint8_t)(RS_ST_FAST << 5);
@@ -1049,7 +1021,8 @@ extern "C" hipError_t rsk_era(const RsDevTables *tab, const RsCorrParams *prm, c
 {
     if (count == 0)
         return hipSuccess;
-    hipLaunchKernelGGL(rs_era_k, dim3(fast_grid(count, num_cu)), dim3(FWG), 0, stream, tab, *prm, ws->syn, pos8,
+    const size_t need = (count + EWG - 1) / EWG, res = (size_t)(num_cu > 0 ? num_cu : 256) * (ERA_WAVES * 256 / EWG);
+    hipLaunchKernelGGL(rs_era_k, dim3((uint32_t)(need < res ? need : res)), dim3(EWG), 0, stream, tab, *prm, ws->syn, pos8,
                        pos_stride, cnt, count, ws->lam, ws->meta, ws->list, ws->nlist, ok, corrected);
     return hipGetLastError();
 }

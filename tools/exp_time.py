@@ -74,6 +74,10 @@ def child():
     for _ in range(5):
         estep()
     res["erasure_kernels_ms"] = round(sum(ms / c for ms, c in (rs.timing_read(k) for k in P.KERNEL_NAMES) if c), 4)
+    for k in P.KERNEL_NAMES:
+        ms, c = rs.timing_read(k)
+        if c and "erasure" in P.KERNEL_NAMES[k]:
+            res["era_k_ms"] = round(ms / c, 4)
     res["erasure_ok"] = int(ok.sum()) == n
     print(json.dumps(res))
 
