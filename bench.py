@@ -96,7 +96,8 @@ K_ENCODE, K_REMAINDER, K_CORRECT, K_CHECK, K_BM, K_CHIEN, K_FORNEY, K_LIST, K_AP
 PATHS = {
     "encode": (K_ENCODE,),
     "decode16": (K_REMAINDER, K_BM, K_CHIEN, K_FORNEY, K_APPLY, K_LIST, K_CORRECT),
-    "erasure32": (K_REMAINDER, K_ERASURE, K_LIST, K_APPLY, K_CORRECT),
+    "erasure32": (K_REMAINDER, K_ERASURE, K_BM, K_CHIEN, K_FORNEY, K_LIST, K_APPLY, K_CORRECT),
+    "errata16e8": (K_REMAINDER, K_ERASURE, K_BM, K_CHIEN, K_FORNEY, K_LIST, K_APPLY, K_CORRECT),
 }
 
 
@@ -446,12 +447,26 @@ def run_weak(be, ranks, args, rank, world):
             "checksum": ranks.sum_u64(csum), "cw": cw, "clean": clean, "err": err, "st": st}
 
 
-def run_erasure(be, ranks, args, rank, world, w):
-    """configs[3]: 32 sorted erasures per codeword in [0, 223), positions passed per codeword."""
+def run_erasure(be, ranks, args, rank, world, w, ne=32, nerr=0):
+    """configs[3]: 32 sorted erasures per codeword in [0, 223), positions passed
+    per codeword.  ne < 32 (the errata kernels): ne + nerr sorted unique
+    positions in the message, every third one an error (not on the list),
+    the rest the ne erasure slots; the stale slots past the count are 0, so
+    the reference's slot-by-root-ordinal apply (src/decode.c:211-214) leaves
+    these codewords changed, not restored: verified = ok and corrected_num
+    (ne + nerr) for every codeword, the bytes by the GPU tests against the
+    oracle (tests/test_gpu_split.py::test_errata_*)."""
     B = args.batch
     first = rank * B
-    slots, emag = be.errors(first, B, 32, K, SEED + 2, sorted_positions=True)
-    cnts = be.counts(B, 32)
+    tot = ne + nerr
+    pos, emag = be.errors(first, B, tot, K, SEED + 2 + (0 if ne == 32 else 7), sorted_positions=True)
+    if nerr:
+        keep = [k for k in range(tot) if k % 3 != 2][:ne] if nerr * 3 >= tot else list(range(ne))
+        slots = be.torch.zeros((B, 32), dtype=be.torch.uint8, device=be.dev)
+        slots[:, :ne] = pos[:, keep]
+    else:
+        slots = pos
+    cnts = be.counts(B, ne)
     cw = w["cw"]
     be.encode(cw)
     eclean = be.like(cw)
@@ -463,14 +478,14 @@ def run_erasure(be, ranks, args, rank, world, w):
         for _ in range(es + 1):
             b = be.like(cw)
             be.copy(b, eclean)
-            be.channel(b, (slots, emag))
+            be.channel(b, (pos, emag))
             ebad.append(b)
 
     def estep(k):
         if ecopies:
             d = ebad[k]
         else:
-            be.channel(cw, (slots, emag))
+            be.channel(cw, (pos, emag))
             d = cw
         be.decode(d, w["st"], erasures=(slots, cnts))
 
@@ -486,11 +501,14 @@ def run_erasure(be, ranks, args, rank, world, w):
     ekt = {k: v for k, v in ekt.items() if v[1]}
     kms = sum(ms / es for ms, n in ekt.values())
     be.rs.timing(False)
-    enbad = be.n_bad(w["st"], 32) + sum(be.n_diff(b, eclean) for b in (ebad[1:] if ecopies else [cw]))
+    enbad = be.n_bad(w["st"], tot)
+    if not nerr:
+        enbad += sum(be.n_diff(b, eclean) for b in (ebad[1:] if ecopies else [cw]))
     enbad = ranks.sum_int(enbad)
     return {"cw_per_s": round(B * world * es / et, 1),
             "kernel_cw_per_s_per_gpu": round(B / (kms * 1e-3), 1) if kms else None,
             "kernels_avg_ms": {be.P.KERNEL_NAMES[k]: round(ms / n, 4) for k, (ms, n) in ekt.items()},
+            "erasures": ne, "errors": nerr,
             "positions_bytes_per_cw": 32,
             "verified": enbad == 0,
             "channel": "outside the timed decodes (one corrupted copy per decode)" if ecopies
@@ -756,6 +774,9 @@ def main(argv=None):
             era = run_erasure(be, ranks, args, rank, world, w)
             modes["erasure32"] = path_roofline("erasure32", era.pop("_kt"), era.pop("_steps"), B, traffic)
             line["erasure_decode_32"] = era
+            eta = run_erasure(be, ranks, args, rank, world, w, ne=16, nerr=8)
+            modes["errata16e8"] = path_roofline("errata16e8", eta.pop("_kt"), eta.pop("_steps"), B, traffic)
+            line["errata_decode_16e8"] = eta
             line["verified"] = line["verified"] and era["verified"]
         rt_ms = modes["encode"]["path_ms"] + modes["decode16"]["path_ms"]
         rt = 2 * B * CW_BYTES / (rt_ms * 1e-3) / 1e9

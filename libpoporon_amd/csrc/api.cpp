@@ -496,7 +496,7 @@ static void build_tables(poporon_t *h)
         }
     }
     /* Chien chunk rows: term j at 16 consecutive points */
-    for (uint32_t j = 1; j <= 16; j++) {
+    for (uint32_t j = 1; j <= 32; j++) {
         for (uint32_t e = 0; e < 256; e++) {
             uint8_t rowb[16];
             for (uint32_t b = 0; b < 16; b++)
@@ -1201,32 +1201,56 @@ static bool launch_decode(poporon_t *h, uint8_t *d_data, size_t ds, uint8_t *d_p
             return false;
         return !shared || rem_release(g, s);
     }
-    /* erasure batches: the general kernel's decode with the corrections as
-     * records, applied block-wise (scattered byte read-modify-writes cost
-     * ~0.3 ms per 2^20 codewords with 32 erasures) */
+    /* erasure batches: records (64 B per codeword in ws.ext) applied
+     * block-wise (scattered byte read-modify-writes cost ~0.3 ms per 2^20
+     * codewords with 32 erasures).  u8 slots: rs_era_k for 32 sorted
+     * erasures (prim 1), the errata kernels (rs_errata.hip) for every other
+     * count with or without errors, the general kernel's list for what they
+     * hand on; u32 slots: the general kernel for all */
     const bool esplit = !ext_syn && (pos8 || pos32) && prm.vfast && !prm.force_verify &&
                         h->decode_path != 2 && (h->decode_path == 1 || count >= SPLIT_MIN_COUNT);
     if (esplit) {
         const RsSplitWs ws = rs_ws_carve(rem, rem_cap ? rem_cap : count);
         GpuCtx &g = h->gpu;
-        /* 32 sorted erasures (prim 1): rs_era_k, the rest through the list */
-        const bool efast = pos8 && prm.prim == 1u && pos_stride % 16u == 0u &&
-                           (reinterpret_cast<uintptr_t>(pos8) & 15u) == 0u;
-        if (efast) {
+        const uintptr_t pa = reinterpret_cast<uintptr_t>(pos8);
+        const bool efast = pos8 && prm.prim == 1u && pos_stride % 16u == 0u && (pa & 15u) == 0u;
+        const bool errata = pos8 && pos_stride >= RS_NR && pos_stride % 4u == 0u && (pa & 3u) == 0u;
+        if (efast || errata) {
             {
                 KernelTimer t(g, POPORON_AMD_KERNEL_REMAINDER, s);
                 HIP_OK(rsk_syndrome_reset(g.tab, d_data, ds, d_par, ps, (uint32_t)size, count, ws.syn, ws.nlist,
                                           g.num_cu, s));
                 t.done();
             }
-            {
+            if (efast) {
                 KernelTimer t(g, POPORON_AMD_KERNEL_ERASURE, s);
-                HIP_OK(rsk_era(g.tab, &prm, &ws, pos8, pos_stride, cnt, count, ok, corrected, g.num_cu, s));
+                HIP_OK(rsk_era(g.tab, &prm, &ws, pos8, pos_stride, cnt, count, ok, corrected, errata ? 1u : 0u,
+                               g.num_cu, s));
                 t.done();
+            }
+            if (errata) {
+                const uint32_t only_pend = efast ? 1u : 0u;
+                {
+                    KernelTimer t(g, POPORON_AMD_KERNEL_BM, s);
+                    HIP_OK(rsk_ebm(g.tab, &prm, &ws, pos8, pos_stride, cnt, count, ok, corrected, only_pend, g.num_cu,
+                                   s));
+                    t.done();
+                }
+                {
+                    KernelTimer t(g, POPORON_AMD_KERNEL_CHIEN, s);
+                    HIP_OK(rsk_chien32(g.tab, &prm, &ws, count, ok, corrected, only_pend, g.num_cu, s));
+                    t.done();
+                }
+                {
+                    KernelTimer t(g, POPORON_AMD_KERNEL_FORNEY, s);
+                    HIP_OK(rsk_forney32(g.tab, &prm, &ws, pos8, pos_stride, count, ok, corrected, only_pend,
+                                        g.num_cu, s));
+                    t.done();
+                }
             }
             {
                 KernelTimer t(g, POPORON_AMD_KERNEL_LIST, s);
-                HIP_OK(rsk_correct_era_list(g.tab, &prm, count, ws.syn, pos8, pos_stride, cnt, ok, corrected, ws.lam,
+                HIP_OK(rsk_correct_era_list(g.tab, &prm, count, ws.syn, pos8, pos_stride, cnt, ok, corrected, ws.ext,
                                             ws.meta, ws.list, ws.nlist, g.num_cu, s));
                 t.done();
             }
@@ -1237,13 +1261,13 @@ static bool launch_decode(poporon_t *h, uint8_t *d_data, size_t ds, uint8_t *d_p
                 t.done();
             }
             KernelTimer t(g, POPORON_AMD_KERNEL_CORRECT, s);
-            HIP_OK(rsk_correct_era_rec(g.tab, &prm, count, ws.syn, pos8, pos32, pos_stride, cnt, ok, corrected, ws.lam,
+            HIP_OK(rsk_correct_era_rec(g.tab, &prm, count, ws.syn, pos8, pos32, pos_stride, cnt, ok, corrected, ws.ext,
                                        ws.meta, g.num_cu, s));
             t.done();
         }
         {
             KernelTimer t(g, POPORON_AMD_KERNEL_APPLY, s);
-            HIP_OK(rsk_apply_era(&prm, ws.meta, ws.lam, d_data, ds, d_par, ps, count, s));
+            HIP_OK(rsk_apply_era(&prm, ws.meta, ws.ext, d_data, ds, d_par, ps, count, s));
             t.done();
         }
         return !shared || rem_release(g, s);

@@ -42,8 +42,9 @@ struct RsDevTables {
     uint4 synt[32 * 2 * 2 * 16];
     /* chien[(j-1)*256 + e] = 16 bytes alpha^(e + j*b), b = 0..15: the j-th
      * locator term at 16 consecutive points for a coefficient of log e;
-     * entry e = 255 (log of zero) is an all-zero row. */
-    uint4 chien[16 * 256];
+     * entry e = 255 (log of zero) is an all-zero row.  Terms 1..16 serve
+     * the error-mode kernels, 1..32 the errata Chien search. */
+    uint4 chien[32 * 256];
     /* gfa: the LDS image of the split kernels' GF table (rs_fast.hip header),
      * dword x * 32 + r for x < 512 and replica r < 32:
      *   (exp2[x] << 8) | (la << 16),  la = 128 log x + 4r + 1 for 0 < x < 256,
@@ -85,16 +86,23 @@ struct RsCorrParams {
  *   om    16 B  log Omega_0..15 (255 = zero)             (rsk_bm)
  *   roots 32 B  root map over the points alpha^i', i' = 0..255 (rsk_chien),
  *               then the corrections: 16 locations, 16 magnitudes (rsk_forney)
- *   meta   1 B  state << 5 | deg(Lambda)                 (rsk_bm, rsk_chien)
+ *   ext   64 B  errata decode (rs_errata.hip): log Lambda_1..32 || log
+ *               Omega_0..31 (rsk_ebm), then the 64-byte correction record
+ *               (rsk_forney32, rsk_correct_era_list)
+ *   meta   1 B  state << 5 | deg(Lambda)                 (rsk_bm, rsk_chien;
+ *               errata: deg & 31, 0 meaning 32)
  *   list   4 B  codewords handed to the general kernel (rsk_correct_list)
- *   nlist  the list's length (zeroed by rsk_syndrome)
+ *   nlist  the list's length, then the count of RS_ST_PEND codewords (both
+ *          zeroed by rsk_syndrome_reset)
  */
 #define RS_ST_DONE 0u /* ok / corrected written */
 #define RS_ST_FAST 1u /* deg(Lambda) = L <= 16: Chien, then Forney */
 #define RS_ST_LIST 2u /* on the list: the general kernel decodes it */
+#define RS_ST_PEND 3u /* erasure mode: left by rs_era_k for the errata kernels */
+#define RS_ST_ERRATA 4u /* errata decode: deg(Lambda) = L (deg & 31), Chien and Forney next */
 
 struct RsSplitWs {
-    uint8_t *syn, *lam, *om, *roots, *meta;
+    uint8_t *syn, *lam, *om, *roots, *ext, *meta;
     uint32_t *list, *nlist;
 };
 
@@ -102,7 +110,7 @@ static inline size_t rs_ws_round16(size_t n) { return (n + 15) & ~(size_t)15; }
 
 static inline size_t rs_ws_bytes(size_t cap)
 {
-    return 96 * cap + rs_ws_round16(cap) + rs_ws_round16(4 * cap) + 16;
+    return 160 * cap + rs_ws_round16(cap) + rs_ws_round16(4 * cap) + 16;
 }
 
 static inline RsSplitWs rs_ws_carve(uint8_t *base, size_t cap)
@@ -112,7 +120,8 @@ static inline RsSplitWs rs_ws_carve(uint8_t *base, size_t cap)
     w.lam = w.syn + 32 * cap;
     w.om = w.lam + 16 * cap;
     w.roots = w.om + 16 * cap;
-    w.meta = w.roots + 32 * cap;
+    w.ext = w.roots + 32 * cap;
+    w.meta = w.ext + 64 * cap;
     w.list = (uint32_t *)(w.meta + rs_ws_round16(cap));
     w.nlist = (uint32_t *)((uint8_t *)w.list + rs_ws_round16(4 * cap));
     return w;
@@ -217,24 +226,49 @@ hipError_t rsk_apply(const RsCorrParams *prm, const RsSplitWs *ws, uint8_t *data
  *                        positions clamped to 255, 32 magnitudes) into rec,
  *                        meta[cw] = RS_ST_FAST where a record was written
  *   rsk_apply_era        the records into the codewords (rs_apply_k<32>)
- * rec: the 64 * cap bytes from ws.lam (lam, om and roots back to back).
+ * rec: ws.ext.
  */
 hipError_t rsk_correct_era_rec(const RsDevTables *tab, const RsCorrParams *prm, size_t count, const uint8_t *syn,
                                const uint8_t *pos8, const uint32_t *pos32, size_t pos_stride, const uint8_t *cnt,
                                uint8_t *ok, uint8_t *corrected, uint8_t *rec, uint8_t *meta, int num_cu,
                                hipStream_t stream);
 /* the 32-sorted-erasure kernel (rs_fast.hip: rs_era_k, prim 1, 16-byte
- * aligned u8 slots): records for its codewords, clean ones finished, the rest
- * onto ws.list (zeroed by rsk_syndrome_reset) for rsk_correct_era_list */
+ * aligned u8 slots): records (ws.ext) for its codewords, clean ones finished,
+ * the rest RS_ST_PEND for the errata kernels (pend != 0) or onto ws.list
+ * (zeroed by rsk_syndrome_reset) for rsk_correct_era_list */
 hipError_t rsk_era(const RsDevTables *tab, const RsCorrParams *prm, const RsSplitWs *ws, const uint8_t *pos8,
-                   size_t pos_stride, const uint8_t *cnt, size_t count, uint8_t *ok, uint8_t *corrected, int num_cu,
-                   hipStream_t stream);
+                   size_t pos_stride, const uint8_t *cnt, size_t count, uint8_t *ok, uint8_t *corrected, uint32_t pend,
+                   int num_cu, hipStream_t stream);
 hipError_t rsk_correct_era_list(const RsDevTables *tab, const RsCorrParams *prm, size_t count, const uint8_t *syn,
                                 const uint8_t *pos8, size_t pos_stride, const uint8_t *cnt, uint8_t *ok,
                                 uint8_t *corrected, uint8_t *rec, uint8_t *meta, const uint32_t *list,
                                 const uint32_t *list_n, int num_cu, hipStream_t stream);
 hipError_t rsk_apply_era(const RsCorrParams *prm, const uint8_t *meta, const uint8_t *rec, uint8_t *data,
                          size_t dstride, uint8_t *parity, size_t pstride, size_t count, hipStream_t stream);
+
+/*
+ * Split errata decode (rs_errata.hip): erasure mode with any count of u8
+ * slots (pos_stride >= 32, 4-byte aligned rows) and errors, after
+ * rsk_syndrome_reset into ws.syn:
+ *   rsk_ebm      erasure locator + Berlekamp-Massey from r = count + 1 + Omega
+ *                -> ws.ext (logs), ws.meta (RS_ST_ERRATA); clean codewords
+ *                finished; deg != L, count > 32 or slots past the codeword ->
+ *                ws.list.  only_pend: just the RS_ST_PEND codewords rsk_era left
+ *   rsk_chien32  roots of Lambda (degree <= 32) -> ws.roots; count != deg
+ *                finished (failure)
+ *   rsk_forney32 magnitudes -> ws.ext as 64-byte records (root n's magnitude
+ *                with list slot n, as the reference applies them), ok / corrected
+ * then rsk_correct_era_list over ws.list (records into ws.ext) and
+ * rsk_apply_era(ws.meta, ws.ext).
+ */
+hipError_t rsk_ebm(const RsDevTables *tab, const RsCorrParams *prm, const RsSplitWs *ws, const uint8_t *pos8,
+                   size_t pos_stride, const uint8_t *cnt, size_t count, uint8_t *ok, uint8_t *corrected,
+                   uint32_t only_pend, int num_cu, hipStream_t stream);
+hipError_t rsk_chien32(const RsDevTables *tab, const RsCorrParams *prm, const RsSplitWs *ws, size_t count, uint8_t *ok,
+                       uint8_t *corrected, uint32_t only_pend, int num_cu, hipStream_t stream);
+hipError_t rsk_forney32(const RsDevTables *tab, const RsCorrParams *prm, const RsSplitWs *ws, const uint8_t *pos8,
+                        size_t pos_stride, size_t count, uint8_t *ok, uint8_t *corrected, uint32_t only_pend,
+                        int num_cu, hipStream_t stream);
 
 #ifdef __cplusplus
 }

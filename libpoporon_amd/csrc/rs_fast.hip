@@ -607,7 +607,8 @@ __global__ __launch_bounds__(EWG, ERA_WAVES) void rs_era_k(const RsDevTables *__
                                                          const uint8_t *__restrict__ cntp, size_t count,
                                                          uint8_t *__restrict__ rec, uint8_t *__restrict__ meta,
                                                          uint32_t *__restrict__ list, uint32_t *__restrict__ nlist,
-                                                         uint8_t *__restrict__ ok, uint8_t *__restrict__ corrected)
+                                                         uint8_t *__restrict__ ok, uint8_t *__restrict__ corrected,
+                                                         uint32_t pend)
 {
     __shared__ uint32_t lgf[512 * 32];
     fill_gfa<EWG>(lgf, T);
@@ -650,11 +651,16 @@ __global__ __launch_bounds__(EWG, ERA_WAVES) void rs_era_k(const RsDevTables *__
                 if (corrected)
                     corrected[cw] = 0;
                 meta[cw] = (uint8_t)(RS_ST_DONE << 5);
+            } else if (pend) { /* the errata kernels (rs_errata.hip) decode it */
+                meta[cw] = (uint8_t)(RS_ST_PEND << 5);
             } else {
                 meta[cw] = (uint8_t)(RS_ST_LIST << 5);
                 list[atomicAdd(nlist, 1u)] = (uint32_t)cw;
             }
         }
+        const uint64_t pw = __ballot(valid && any && !fast && pend);
+        if (pw != 0ull && (threadIdx.x & 63u) == (uint32_t)__builtin_ctzll(pw))
+            nlist[1] = 1u; /* the errata kernels run only if some codeword is pending: one store per wave */
         if (__ballot(fast) == 0ull) /* uniform */
             continue;
         uint32_t *recw = reinterpret_cast<uint32_t *>(rec + (valid ? cw : 0) * 64u);
@@ -1017,12 +1023,12 @@ extern "C" hipError_t rsk_apply_era(const RsCorrParams *prm, const uint8_t *meta
 
 extern "C" hipError_t rsk_era(const RsDevTables *tab, const RsCorrParams *prm, const RsSplitWs *ws, const uint8_t *pos8,
                               size_t pos_stride, const uint8_t *cnt, size_t count, uint8_t *ok, uint8_t *corrected,
-                              int num_cu, hipStream_t stream)
+                              uint32_t pend, int num_cu, hipStream_t stream)
 {
     if (count == 0)
         return hipSuccess;
     const size_t need = (count + EWG - 1) / EWG, res = (size_t)(num_cu > 0 ? num_cu : 256) * (ERA_WAVES * 256 / EWG);
     hipLaunchKernelGGL(rs_era_k, dim3((uint32_t)(need < res ? need : res)), dim3(EWG), 0, stream, tab, *prm, ws->syn, pos8,
-                       pos_stride, cnt, count, ws->lam, ws->meta, ws->list, ws->nlist, ok, corrected);
+                       pos_stride, cnt, count, ws->ext, ws->meta, ws->list, ws->nlist, ok, corrected, pend);
     return hipGetLastError();
 }

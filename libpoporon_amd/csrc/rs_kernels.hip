@@ -414,8 +414,10 @@ __global__ __launch_bounds__(LFSR_WG) void rs_lfsr_k(const RsDevTables *__restri
                                                       size_t count, uint8_t *__restrict__ out,
                                                       uint32_t *__restrict__ reset)
 {
-    if (reset && blockIdx.x == 0 && threadIdx.x == 0)
-        *reset = 0u; /* the split decode's list length, before any later launch on the stream */
+    if (reset && blockIdx.x == 0 && threadIdx.x == 0) {
+        reset[0] = 0u; /* the split decode's list length, before any later launch on the stream */
+        reset[1] = 0u; /* and the erasure decode's count of codewords left to the errata kernels */
+    }
     __shared__ uint4 lds[512 * LFSR_REPL + (MODE == MODE_SYNDROME ? 32 * 2 * 2 * 16 : 0)];
     for (uint32_t t = threadIdx.x; t < 512u * LFSR_REPL; t += LFSR_WG)
         lds[t] = T->lfsr[t / LFSR_REPL];

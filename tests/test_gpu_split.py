@@ -295,3 +295,124 @@ def test_erasure_count_past_roots(monkeypatch, oracle_default, path):
     want = oracle_default.decode_batch(cw[inr, :223], cw[inr, 223:], slots[inr].astype(np.uint32),
                                        cnt[inr].astype(np.uint32))
     _same((ok[inr], cor[inr], d[inr], p[inr]), want)
+
+
+def _errata_batch(rng, h, n, size, ne, nerr, sort=True, mag=None):
+    """ne erasures (slots in the message, sorted or in insertion order, stale
+    slots after the count) and 0..nerr errors elsewhere in each codeword."""
+    data = rng.integers(0, 256, (n, size), dtype=np.uint8)
+    cw = np.concatenate([data, h.encode_batch(data)], 1)
+    L = size + NR
+    slots = np.zeros((n, NR), np.uint8)
+    cnt = np.full(n, ne, np.uint8)
+    for c in range(n):
+        er = rng.permutation(size)[:ne]
+        if sort:
+            er = np.sort(er)
+        slots[c, :ne] = er
+        slots[c, ne:] = rng.integers(0, L, NR - ne)  # stale entries past the count (quirk Q1)
+        cw[c, er] ^= rng.integers(1, 256, ne, dtype=np.uint8) if mag is None else np.uint8(mag)
+        x = int(rng.integers(0, nerr + 1))
+        rest = np.setdiff1d(np.arange(L), er)
+        cw[c, rng.permutation(rest)[:x]] ^= rng.integers(1, 256, x, dtype=np.uint8)
+    return cw, slots, cnt
+
+
+@pytest.mark.parametrize("path", PATHS)
+@pytest.mark.parametrize("size,ne,nerr,sort,mag", [
+    (223, 16, 8, True, None),   # errors and erasures: the errata kernels' target case
+    (223, 16, 0, False, 0xFF),  # tests/test_codec.c:123-168: 16 erasures in insertion order, magnitude 0xFF
+    (64, 20, 0, False, 0xFF),   # tests/test_unified.c:82-112: 20 erasures in a 64-byte message
+    (223, 24, 4, True, None),
+    (223, 8, 12, False, None),
+    (200, 16, 8, True, None),
+    (223, 31, 0, True, None),
+    (223, 1, 15, True, None)])
+def test_errata_vs_oracle(monkeypatch, oracle_default, path, size, ne, nerr, sort, mag):
+    """Erasure counts below 32 with errors besides (rs_ebm_k, rs_chien32_k,
+    rs_forney32_k, then the record apply) and the single kernel, bit for bit
+    against the oracle -- including the reference's own erasure test cases,
+    whose codewords come back restored."""
+    h = _handle(monkeypatch, path)
+    rng = np.random.default_rng(700 + size + ne * 3 + nerr)
+    cw, slots, cnt = _errata_batch(rng, h, 10000, size, ne, nerr, sort, mag)
+    got = h.decode_batch(cw[:, :size], cw[:, size:], slots, cnt)
+    want = oracle_default.decode_batch(cw[:, :size], cw[:, size:], slots.astype(np.uint32), cnt.astype(np.uint32))
+    assert want[0].sum() > 9000
+    _same(got, want)
+    if mag is not None:  # the reference tests' assertion: the message is restored
+        assert got[0].all()
+
+
+def test_errata_kernels_timed(monkeypatch, torch_cuda_split):
+    """2^16 codewords with 16 sorted erasures and 8 errors each on the device
+    API: rs_era_k leaves them pending, the errata kernels decode them, the
+    general kernel never runs; ok / corrected for all, bytes of a sample
+    against the oracle."""
+    torch = torch_cuda_split
+    from oracle import Oracle
+    o = Oracle(8, 0x11D, 1, 1, 32)
+    h = _handle(monkeypatch, "split")
+    n = 1 << 16
+    g = torch.Generator(device="cuda")
+    g.manual_seed(11)
+    cw = torch.randint(0, 256, (n, 255), dtype=torch.uint8, device="cuda", generator=g)
+    s = torch.cuda.current_stream().cuda_stream
+    base = cw.data_ptr()
+    h.encode_batch_device(base, 255, base + 223, 255, 223, n, s)
+    r = torch.rand((n, 255), device="cuda", generator=g)
+    era = r[:, :223].topk(16, dim=1).indices.sort(dim=1).values  # erasures in the message
+    pos = r.scatter(1, era, -1.0).topk(8, dim=1).indices  # errors anywhere else
+    mag = torch.randint(1, 256, (n, 16), dtype=torch.uint8, device="cuda", generator=g)
+    cw.scatter_(1, era, cw.gather(1, era) ^ mag)
+    emag = torch.randint(1, 256, (n, 8), dtype=torch.uint8, device="cuda", generator=g)
+    cw.scatter_(1, pos, cw.gather(1, pos) ^ emag)
+    slots = torch.zeros((n, NR), dtype=torch.uint8, device="cuda")
+    slots[:, :16] = era.to(torch.uint8)
+    cnt = torch.full((n,), 16, dtype=torch.uint8, device="cuda")
+    before = cw.cpu().numpy()
+    ok = torch.zeros(n, dtype=torch.uint8, device="cuda")
+    cor = torch.zeros(n, dtype=torch.uint8, device="cuda")
+    h.timing(True)
+    h.decode_batch_device(base, 255, base + 223, 255, 223, n, ok.data_ptr(), cor.data_ptr(),
+                          d_positions=slots.data_ptr(), positions_stride=NR, d_counts=cnt.data_ptr(), stream=s)
+    torch.cuda.synchronize()
+    t = {k: h.timing_read(k) for k in P.KERNEL_NAMES}
+    h.timing(False)
+    for k in (P.KERNEL_REMAINDER, P.KERNEL_ERASURE, P.KERNEL_BM, P.KERNEL_CHIEN, P.KERNEL_FORNEY, P.KERNEL_LIST,
+              P.KERNEL_APPLY):
+        assert t[k][1] == 1, (k, t[k])
+    assert t[P.KERNEL_CORRECT][1] == 0
+    assert int(ok.sum()) == n
+    sel = np.arange(0, n, 29)
+    sl = slots.cpu().numpy()[sel].astype(np.uint32)
+    want = o.decode_batch(before[sel, :223], before[sel, 223:], sl, np.full(sel.size, 16, np.uint32))
+    out = cw.cpu().numpy()[sel]
+    _same((ok.cpu().numpy()[sel], cor.cpu().numpy()[sel], out[:, :223], out[:, 223:]), want)
+
+
+@pytest.mark.parametrize("stride", [32, 40, 33])
+def test_errata_slot_strides(monkeypatch, oracle_default, torch_cuda_split, stride):
+    """Slot rows 32 (rs_era_k + errata), 40 (errata alone: not 16-byte rows)
+    and 33 bytes apart (unaligned rows: the general kernel) give the same
+    answers, equal to the oracle's."""
+    torch = torch_cuda_split
+    h = _handle(monkeypatch, "split")
+    rng = np.random.default_rng(stride)
+    cw, slots, cnt = _errata_batch(rng, h, 9000, 223, 12, 10, sort=bool(stride & 1))
+    want = oracle_default.decode_batch(cw[:, :223], cw[:, 223:], slots.astype(np.uint32), cnt.astype(np.uint32))
+    n = cw.shape[0]
+    d = torch.from_numpy(cw.copy()).cuda()
+    sl = np.zeros((n, stride), np.uint8)
+    sl[:, :NR] = slots
+    sd = torch.from_numpy(sl.reshape(-1)).cuda()
+    cd = torch.from_numpy(cnt).cuda()
+    ok = torch.zeros(n, dtype=torch.uint8, device="cuda")
+    cor = torch.zeros(n, dtype=torch.uint8, device="cuda")
+    s = torch.cuda.current_stream().cuda_stream
+    base = d.data_ptr()
+    h.decode_batch_device(base, 255, base + 223, 255, 223, n, ok.data_ptr(), cor.data_ptr(),
+                          d_positions=sd.data_ptr(), positions_stride=stride, d_counts=cd.data_ptr(), stream=s)
+    torch.cuda.synchronize()
+    out = d.cpu().numpy()
+    _same((ok.cpu().numpy(), cor.cpu().numpy(), out[:, :223], out[:, 223:]), want)
