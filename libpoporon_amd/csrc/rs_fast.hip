@@ -779,7 +779,7 @@ __global__ __launch_bounds__(EWG, ERA_WAVES) void rs_era_k(const RsDevTables *__
          * Omega_m alpha^(i m), den = sum_h Lambda_(2h+1) alpha^(2h i),
          * magnitude alpha^(log num + log alpha^(i (fcr-1)) + 255 - log den);
          * a zero numerator corrects nothing and is not counted ---- */
-        uint32_t ncor = 0;
+        uint32_t ncor = 0, mrec[RS_NR / 4];
         const uint32_t *slw = reinterpret_cast<const uint32_t *>(slots);
         uint32_t opu[RS_NR], alou[RS_NR / 2]; /* unpacked once: plain adds in the loop, not SDWA word selects */
 #pragma unroll
@@ -843,13 +843,19 @@ __global__ __launch_bounds__(EWG, ERA_WAVES) void rs_era_k(const RsDevTables *__
                 ncor += z ? 1u : 0u;
                 cur[t >> 2] |= (z ? gf.exp((lnum + ln2 + RS_NN - lden) % 255u) : 0u) << (8 * (t & 3));
             }
-            if (fast) {
+            /* magnitude words through a shift register: the record's 32
+             * bytes go out as two 16-byte stores (eight dword stores per
+             * record cost ~130 B of partial-line writes per codeword) */
 #pragma unroll
-                for (int k = 0; k < ERA_R / 4; ++k)
-                    recw[8 + q * (ERA_R / 4) + k] = cur[k];
-            }
+            for (int k = 0; k < RS_NR / 4 - ERA_R / 4; ++k)
+                mrec[k] = mrec[k + ERA_R / 4];
+#pragma unroll
+            for (int k = 0; k < ERA_R / 4; ++k)
+                mrec[RS_NR / 4 - ERA_R / 4 + k] = cur[k];
         }
         if (fast) {
+            reinterpret_cast<uint4 *>(recw)[2] = make_uint4(mrec[0], mrec[1], mrec[2], mrec[3]);
+            reinterpret_cast<uint4 *>(recw)[3] = make_uint4(mrec[4], mrec[5], mrec[6], mrec[7]);
             meta[cw] = (uint8_t)(RS_ST_FAST << 5);
             ok[cw] = 1;
             if (corrected)

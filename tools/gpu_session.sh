@@ -42,7 +42,7 @@ for step in "$@"; do
     traffic)
         # HBM bytes per codeword of each bench path: FETCH_SIZE and WRITE_SIZE
         # in separate passes per driver mode (tools/pmc_traffic.py)
-        for mode in roundtrip erasure; do
+        for mode in roundtrip erasure errata; do
             for c in FETCH_SIZE WRITE_SIZE; do
                 lc=$(echo $c | cut -d_ -f1 | tr A-Z a-z)
                 run traffic_${mode}_$lc 150 rocprofv3 --pmc $c -d gpurun_out/traffic/${mode}_$lc -o pmc \

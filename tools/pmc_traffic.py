@@ -4,7 +4,7 @@
     python tools/pmc_traffic.py gpurun_out/traffic --json profiles/traffic_latest.json
 
 Expects <dir>/<mode>_fetch/*counter_collection.csv and <dir>/<mode>_write/...
-for mode in {roundtrip, erasure}: one `rocprofv3 --pmc FETCH_SIZE` and one
+for mode in {roundtrip, erasure, errata}: one `rocprofv3 --pmc FETCH_SIZE` and one
 `--pmc WRITE_SIZE` pass (never together with tracing; tools/gpu_session.sh
 step `traffic`) over `tools/kernel_driver.py --mode <mode> --n N`.
 
@@ -13,7 +13,8 @@ Per kernel dispatch (MI355X_MICROARCH.md "HBM"):
     write bytes = WRITE_SIZE (KB) x 1024
 averaged over the dispatches of each kernel, divided by the codewords of a
 dispatch, and summed over the kernels of each bench path (bench.PATHS):
-encode (roundtrip run), decode16 (roundtrip run), erasure32 (erasure run).
+encode (roundtrip run), decode16 (roundtrip run), erasure32 (erasure run),
+errata16e8 (errata run).
 The output is stamped with bench.source_stamp(): bench.py ignores a file
 whose stamp does not match the kernel sources it runs.
 """
@@ -35,7 +36,8 @@ import bench  # noqa: E402
 # rocprof kernel name -> bench kernel id (include/poporon_amd.h)
 PATTERNS = [
     (r"rs_lfsr_k<0,", bench.K_ENCODE), (r"rs_lfsr_k<1,", bench.K_REMAINDER),
-    (r"\brs_bm_k\b", bench.K_BM), (r"\brs_chien_k\b", bench.K_CHIEN), (r"rs_forney_k", bench.K_FORNEY),
+    (r"\brs_bm_k\b|\brs_ebm_k\b", bench.K_BM), (r"\brs_chien_k\b|\brs_chien32_k\b", bench.K_CHIEN),
+    (r"rs_forney_k|rs_forney32_k", bench.K_FORNEY),
     (r"rs_apply_k", bench.K_APPLY), (r"\brs_era_k\b", bench.K_ERASURE),
     (r"rs_correct_k<[^>]*true>|rs_correct_list|rs_correct_k", bench.K_LIST),
 ]
@@ -67,7 +69,7 @@ def main():
     ap.add_argument("--n", type=int, default=1 << 20, help="codewords per dispatch (kernel_driver --n)")
     ap.add_argument("--json", default=None)
     a = ap.parse_args()
-    runs = {"encode": "roundtrip", "decode16": "roundtrip", "erasure32": "erasure"}
+    runs = {"encode": "roundtrip", "decode16": "roundtrip", "erasure32": "erasure", "errata16e8": "errata"}
     out = {"source_stamp": bench.source_stamp(), "date": datetime.datetime.utcnow().strftime("%Y-%m-%d %H:%M UTC"),
            "codewords_per_dispatch": a.n,
            "note": "hbm bytes = FETCH_SIZE x 1024 x 2 + WRITE_SIZE x 1024 per dispatch (MI355X_MICROARCH.md HBM; the "
