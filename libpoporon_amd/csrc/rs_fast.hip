@@ -380,20 +380,25 @@ __global__ __launch_bounds__(FWG, 8) void rs_chien_k(const RsDevTables *__restri
                     acc[2] = xor3(acc[2], r1.z, r2.z);
                     acc[3] = xor3(acc[3], r1.w, r2.w);
                 }
-                word |= zero_bytes16(acc) << (16 * h);
+                /* zero bytes as flags: point 16h + 4d + b (byte b of dword d)
+                 * at bit 8b + 7 - d - 4h -- shifts and 3-way ORs, no
+                 * multiplies; error mode needs the roots in no order */
+#pragma unroll
+                for (int d = 0; d < 4; ++d)
+                    word = __builtin_amdgcn_bitop3_b32(word, zero80(acc[d]) >> (d + 4 * h), 0u, 0xF0 | 0xCC);
             }
             if (w == 7)
-                word &= 0x7FFFFFFFu; /* i' = 255 repeats i' = 0 */
+                word &= ~(1u << 24); /* i' = 255 (point 31: bit 24) repeats i' = 0 */
             if (w == 0) {
-                z0 = word & 1u; /* i' = 0 is the reference's last point, i = 255 */
-                word &= ~1u;
+                z0 = (word >> 7) & 1u; /* i' = 0 (bit 7) is the reference's last point, i = 255 */
+                word &= ~0x80u;
             }
             cnt += __popc(word);
-            const uint32_t wb = 32u * (uint32_t)w;
+            const uint32_t wb = 32u * (uint32_t)w + 28u;
             while (word != 0u) { /* at most deg <= 16 pushes per lane in all */
                 const uint32_t b = __builtin_ctz(word);
                 word &= word - 1u;
-                push(wb + b);
+                push(wb + (b >> 3) - 4u * (b & 7u)); /* bit 8b' + k: point 28 - 4k + b' */
             }
         }
         if (z0)

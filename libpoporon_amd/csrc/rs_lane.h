@@ -101,6 +101,13 @@ __device__ __forceinline__ uint32_t wave_max_full(uint32_t v)
     return __builtin_amdgcn_readlane(x, 63);
 }
 
+/* byte-wise zero test: bit 8b + 7 set iff byte b of v is zero, every other bit clear */
+__device__ __forceinline__ uint32_t zero80(uint32_t v)
+{
+    const uint32_t t = (v & 0x7F7F7F7Fu) + 0x7F7F7F7Fu;
+    return __builtin_amdgcn_bitop3_b32(t, v, 0x7F7F7F7Fu, 0x01); /* ~(t | v | 0x7F7F7F7F) */
+}
+
 /* byte-wise zero test of 16 bytes -> 16-bit mask (bit b: byte b is zero) */
 __device__ __forceinline__ uint32_t zero_bytes16(const uint32_t (&v)[4])
 {
