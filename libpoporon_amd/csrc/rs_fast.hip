@@ -59,10 +59,16 @@
 #define BWG 1024 /* rs_bm_k: 8 waves/SIMD; 4 or 6 measured slower (profiles/r03_bm_experiments.log) */
 #define BM_WAVES 8
 
+/* Grids of up to 8 resident rounds: at 2^20 codewords every workgroup takes
+ * one batch.  A persistent grid (one round, each workgroup looping) measured
+ * 3-6 % slower for rs_bm_k / rs_chien_k / rs_forney_k
+ * (profiles/r03_grid_rounds.log): the oldest waves win the issue arbitration,
+ * finish first, and the last batches run at low occupancy. */
+#define FAST_ROUNDS 8
 static int fast_grid(size_t count, int num_cu)
 {
     const size_t need = (count + FWG - 1) / FWG;
-    const size_t g = 2u * (size_t)(num_cu > 0 ? num_cu : 256);
+    const size_t g = FAST_ROUNDS * 2u * (size_t)(num_cu > 0 ? num_cu : 256);
     return (int)(need < g ? (need ? need : 1) : g);
 }
 
@@ -974,7 +980,8 @@ extern "C" hipError_t rsk_bm(const RsDevTables *tab, const RsSplitWs *ws, size_t
 {
     if (count == 0)
         return hipSuccess;
-    const size_t need = (count + BWG - 1) / BWG, res = (size_t)(num_cu > 0 ? num_cu : 256) * (BM_WAVES * 256 / BWG);
+    const size_t need = (count + BWG - 1) / BWG,
+                 res = FAST_ROUNDS * (size_t)(num_cu > 0 ? num_cu : 256) * (BM_WAVES * 256 / BWG);
     hipLaunchKernelGGL(rs_bm_k, dim3((uint32_t)(need < res ? need : res)), dim3(BWG), 0, stream, tab, ws->syn, count,
                        ws->lam,
                        ws->om, ws->meta, ws->list, ws->nlist, ok, corrected);
@@ -1038,7 +1045,8 @@ extern "C" hipError_t rsk_era(const RsDevTables *tab, const RsCorrParams *prm, c
 {
     if (count == 0)
         return hipSuccess;
-    const size_t need = (count + EWG - 1) / EWG, res = (size_t)(num_cu > 0 ? num_cu : 256) * (ERA_WAVES * 256 / EWG);
+    const size_t need = (count + EWG - 1) / EWG, /* persistent: more rounds measured slower for rs_era_k */
+                 res = (size_t)(num_cu > 0 ? num_cu : 256) * (ERA_WAVES * 256 / EWG);
     hipLaunchKernelGGL(rs_era_k, dim3((uint32_t)(need < res ? need : res)), dim3(EWG), 0, stream, tab, *prm, ws->syn, pos8,
                        pos_stride, cnt, count, ws->ext, ws->meta, ws->list, ws->nlist, ok, corrected, pend);
     return hipGetLastError();
