@@ -80,7 +80,9 @@ __global__ __launch_bounds__(XWG, 4) void rs_ebm_k(const RsDevTables *__restrict
     constexpr uint32_t DQZ = SZ; /* "no update": dq + B's logs read zeros */
     const uint32_t lim = P.size + RS_NR, pad = (uint32_t)P.pad;
 
-    for (size_t base = (size_t)blockIdx.x * XWG; base < count; base += (size_t)gridDim.x * XWG) {
+    uint32_t it = 0;
+    for (size_t base = (size_t)blockIdx.x * XWG; base < count; base += (size_t)gridDim.x * XWG, ++it) {
+        prio_by_progress(it);
         const size_t cw = base + threadIdx.x;
         const bool valid = cw < count && (!only_pend || (meta[cw] >> 5) == RS_ST_PEND);
         const uint32_t *sp = reinterpret_cast<const uint32_t *>(syn + (valid ? cw : 0) * RS_NR);
@@ -322,7 +324,9 @@ __global__ __launch_bounds__(XWG, 4) void rs_chien32_k(const RsDevTables *__rest
     constexpr uint32_t RS = 512u;       /* LDS bytes per e */
     constexpr uint32_t WRAP = 255u * RS;
 
-    for (size_t base = (size_t)blockIdx.x * XWG; base < count; base += (size_t)gridDim.x * XWG) {
+    uint32_t it = 0;
+    for (size_t base = (size_t)blockIdx.x * XWG; base < count; base += (size_t)gridDim.x * XWG, ++it) {
+        prio_by_progress(it);
         const size_t cw = base + threadIdx.x;
         const bool valid = cw < count;
         const uint32_t st = valid ? meta[cw] : 0u;
@@ -476,7 +480,9 @@ __global__ __launch_bounds__(XWG, 4) void rs_forney32_k(const RsDevTables *__res
     __syncthreads();
     const GfA gf{lds_addr(lgf) + 4u * (threadIdx.x & 31u) + 1u};
 
-    for (size_t base = (size_t)blockIdx.x * XWG; base < count; base += (size_t)gridDim.x * XWG) {
+    uint32_t it = 0;
+    for (size_t base = (size_t)blockIdx.x * XWG; base < count; base += (size_t)gridDim.x * XWG, ++it) {
+        prio_by_progress(it);
         const size_t cw = base + threadIdx.x;
         const bool valid = cw < count;
         const uint32_t st = valid ? meta[cw] : 0u;

@@ -632,7 +632,9 @@ __global__ __launch_bounds__(EWG, ERA_WAVES) void rs_era_k(const RsDevTables *__
     auto red7 = [](uint32_t x) __attribute__((always_inline)) { return min(x, x - M255); };
     const uint32_t lim = P.size + RS_NR, pad = (uint32_t)P.pad;
 
-    for (size_t base = (size_t)blockIdx.x * EWG; base < count; base += (size_t)gridDim.x * EWG) {
+    uint32_t it = 0;
+    for (size_t base = (size_t)blockIdx.x * EWG; base < count; base += (size_t)gridDim.x * EWG, ++it) {
+        prio_by_progress(it);
         const size_t cw = base + threadIdx.x;
         const bool valid = cw < count;
         uint4 sa = make_uint4(0, 0, 0, 0), sb = sa, pa = sa, pb = sa;

@@ -35,6 +35,7 @@
 #include <type_traits>
 
 #include "rs_device.h"
+#include "rs_lane.h"
 
 /* global-memory views (global_load, not flat_load) */
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
@@ -77,12 +78,6 @@ __device__ __forceinline__ void il_rows(uint32_t (&R)[8], uint32_t fb, const uin
     const uint4 b = tab[fb * (2 * LFSR_REPL) + LFSR_REPL];
     R[0] = a.x, R[1] = a.y, R[2] = a.z, R[3] = a.w;
     R[4] = b.x, R[5] = b.y, R[6] = b.z, R[7] = b.w;
-}
-
-/* a ^ b ^ c in one VALU op (gfx950 v_bitop3_b32, truth table 0x96) */
-__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c)
-{
-    return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
 }
 
 /* one step at rotation r; d holds the input byte in bits 0..7 (upper bits ignored) */
@@ -353,6 +348,7 @@ __device__ __forceinline__ void store32_any(uint8_t *o, const uint32_t (&P)[8])
         ot[2] = (uint8_t)(t >> 16);
 }
 
+
 #define MODE_ENCODE 0
 #define MODE_SYNDROME 1
 #define MODE_CHECK 2
@@ -435,7 +431,9 @@ __global__ __launch_bounds__(LFSR_WG) void rs_lfsr_k(const RsDevTables *__restri
         for (int k = 0; k < LFSR_STAGGER; ++k)
             __builtin_amdgcn_s_sleep(127);
     if (PATH == PATH_GENERIC) {
-        for (size_t cw = cw0; cw < count; cw += step) {
+        uint32_t it = 0;
+        for (size_t cw = cw0; cw < count; cw += step, ++it) {
+            prio_by_progress(it);
             uint32_t X[8] = {0, 0, 0, 0, 0, 0, 0, 0};
             uint32_t P[8];
             lfsr_feed(X, data + cw * dstride, size, tab);
@@ -451,7 +449,9 @@ __global__ __launch_bounds__(LFSR_WG) void rs_lfsr_k(const RsDevTables *__restri
             sc.load(NextSrc(data + cw0 * dstride, cw0 < count, data));
             __builtin_amdgcn_s_waitcnt(0); /* nothing pending at the loop head but the loop's own refills */
         }
-        for (size_t cw = cw0; cw < count; cw += step) {
+        uint32_t it = 0;
+        for (size_t cw = cw0; cw < count; cw += step, ++it) {
+            prio_by_progress(it);
             const size_t cn = cw + step;
             uint32_t X[8] = {0, 0, 0, 0, 0, 0, 0, 0};
             uint32_t P[8];
@@ -471,7 +471,9 @@ __global__ __launch_bounds__(LFSR_WG) void rs_lfsr_k(const RsDevTables *__restri
             sd.load(NextSrc(data + cw0 * dstride, cw0 < count, data));
             __builtin_amdgcn_s_waitcnt(0); /* nothing pending at the loop head but the loop's own refills */
         }
-        for (size_t cw = cw0; cw < count; cw += step) {
+        uint32_t it = 0;
+        for (size_t cw = cw0; cw < count; cw += step, ++it) {
+            prio_by_progress(it);
             const size_t cn = cw + step;
             const NextSrc dn(data + cn * dstride, cn < count, data + cw * dstride);
             uint32_t X[8] = {0, 0, 0, 0, 0, 0, 0, 0};

@@ -63,6 +63,21 @@ __device__ __forceinline__ uint32_t addmod7(uint32_t x, uint32_t y)
     return r;
 }
 
+/* Persistent loops: issue priority falling with the wave's progress (it =
+ * batches done), so the waves that are behind win the issue arbitration
+ * (priority, then age) and a workgroup's waves finish together instead of
+ * the oldest first, which left the last batches running at low occupancy:
+ * LFSR encode / remainder 5 % faster (profiles/r03_grid_rounds.log). */
+__device__ __forceinline__ void prio_by_progress(uint32_t it)
+{
+    switch (it) {
+    case 0: __builtin_amdgcn_s_setprio(3); break;
+    case 1: __builtin_amdgcn_s_setprio(2); break;
+    case 2: __builtin_amdgcn_s_setprio(1); break;
+    default: __builtin_amdgcn_s_setprio(0); break;
+    }
+}
+
 /* a ^ b ^ c in one VALU op (gfx950 v_bitop3_b32, truth table 0x96) */
 __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c)
 {
