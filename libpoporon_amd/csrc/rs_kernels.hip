@@ -500,6 +500,7 @@ __global__ __launch_bounds__(LFSR_WG) void rs_lfsr_k(const RsDevTables *__restri
     }
 }
 
+
 static int persistent_grid(size_t count, int wg, int num_cu) /* one round: 2 and 4 measured slower (remainder) */
 {
     size_t need = (count + wg - 1) / wg;
