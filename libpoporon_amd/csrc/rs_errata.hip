@@ -304,8 +304,8 @@ __global__ __launch_bounds__(XWG, 4) void rs_ebm_k(const RsDevTables *__restrict
  * is 1 + sum_j row_j[e_j(a)]_b, e_j(a) = (log Lambda_j + 16 a j) mod 255.
  * LDS: row (j, e) at e * 512 + (j - 1) * 16 (128 KiB).  Slot k of lane l
  * holds term ((k + l) mod NT) + 1, so the 16 lanes of a ds_read_b128 group
- * read 16 different bank slots; NT = 16 where the wave's degrees allow (the
- * upper rows' terms are zero).  Roots go into a 32-byte list, newest (largest
+ * read 16 different bank slots; NT = 16 or 24 where the wave's degrees allow
+ * (the upper rows' terms are zero).  Roots go into a 32-byte list, newest (largest
  * i) first.
  */
 __global__ __launch_bounds__(XWG, 4) void rs_chien32_k(const RsDevTables *__restrict__ T, RsCorrParams P,
@@ -352,35 +352,48 @@ __global__ __launch_bounds__(XWG, 4) void rs_chien32_k(const RsDevTables *__rest
                 R[k] = __builtin_amdgcn_alignbyte(R[k], R[k - 1], 3);
             R[0] = (R[0] << 8) | v;
         };
-        auto search = [&](auto ntc) __attribute__((always_inline)) {
-            constexpr int NT = decltype(ntc)::value;
-            constexpr int ND = NT / 4;
-            uint32_t lr = threadIdx.x & (NT - 1);
-            asm volatile("" : "+v"(lr));
-            /* the NT log bytes rotated by lr: byte k of R = log Lambda_(j_k) */
-            uint32_t D[ND];
+        /* the G log bytes of lw from byte b0 rotated by lr (G = 8, 16, 32):
+         * byte k of Rl = log Lambda_(b0 + ((k + lr) mod G) + 1) */
+        auto rotated = [&](auto gc, auto b0c, uint32_t lr, uint32_t *Rl) __attribute__((always_inline)) {
+            constexpr int G = decltype(gc)::value, GD = G / 4, W0 = decltype(b0c)::value / 4;
+            uint32_t D[GD];
 #pragma unroll
-            for (int k = 0; k < ND; ++k)
-                D[k] = lw[k];
+            for (int k = 0; k < GD; ++k)
+                D[k] = lw[W0 + k];
 #pragma unroll
-            for (int bit = 1; bit < ND; bit <<= 1) {
+            for (int bit = 1; bit < GD; bit <<= 1) {
                 const bool c = ((lr >> 2) & (uint32_t)bit) != 0u;
-                uint32_t E[ND];
+                uint32_t E[GD];
 #pragma unroll
-                for (int k = 0; k < ND; ++k)
-                    E[k] = c ? D[(k + bit) % ND] : D[k];
+                for (int k = 0; k < GD; ++k)
+                    E[k] = c ? D[(k + bit) % GD] : D[k];
 #pragma unroll
-                for (int k = 0; k < ND; ++k)
+                for (int k = 0; k < GD; ++k)
                     D[k] = E[k];
             }
-            uint32_t Rl[ND];
 #pragma unroll
-            for (int k = 0; k < ND; ++k)
-                Rl[k] = __builtin_amdgcn_alignbyte(D[(k + 1) % ND], D[k], lr & 3u);
+            for (int k = 0; k < GD; ++k)
+                Rl[k] = __builtin_amdgcn_alignbyte(D[(k + 1) % GD], D[k], lr & 3u);
+        };
+        /* NT slots: NT = 16 or 32 terms rotated by lane mod NT; NT = 24: terms
+         * 1..16 rotated by lane mod 16, 17..24 by lane mod 8 (the last eight
+         * slots read with 2-way bank conflicts: lanes l and l + 8 share a
+         * slot) */
+        auto search = [&](auto ntc) __attribute__((always_inline)) {
+            constexpr int NT = decltype(ntc)::value;
+            constexpr int G1 = NT == 32 ? 32 : 16, G2 = NT - G1;
+            uint32_t lr = threadIdx.x & (G1 - 1);
+            asm volatile("" : "+v"(lr));
+            uint32_t Rl[NT / 4];
+            rotated(std::integral_constant<int, G1>{}, std::integral_constant<int, 0>{}, lr, Rl);
+            if constexpr (G2 > 0)
+                rotated(std::integral_constant<int, G2>{}, std::integral_constant<int, G1>{}, lr & (G2 - 1u),
+                        Rl + G1 / 4);
             uint32_t A[NT], inc[NT];
 #pragma unroll
             for (int k = 0; k < NT; ++k) {
-                const uint32_t jm = ((uint32_t)k + lr) & (NT - 1); /* j - 1 */
+                const uint32_t jm = k < G1 ? (((uint32_t)k + lr) & (G1 - 1))
+                                           : G1 + (((uint32_t)(k - G1) + lr) & (uint32_t)(G2 > 0 ? G2 - 1 : 0)); /* j - 1 */
                 const uint32_t e = (Rl[k >> 2] >> (8 * (k & 3))) & 0xffu;
                 A[k] = cb + e * RS + (jm << 4);
                 inc[k] = e == 255u ? WRAP : ((16u * (jm + 1u)) % 255u) * RS;
@@ -423,8 +436,11 @@ __global__ __launch_bounds__(XWG, 4) void rs_chien32_k(const RsDevTables *__rest
                 push(255u);
             cnt += z0;
         };
-        if (wave_max_full(deg) <= 16u)
+        const uint32_t degmax = wave_max_full(deg);
+        if (degmax <= 16u)
             search(std::integral_constant<int, 16>{});
+        else if (degmax <= 24u)
+            search(std::integral_constant<int, 24>{});
         else
             search(std::integral_constant<int, 32>{});
         bool good = cnt == deg; /* src/decode.c:143-145 */
@@ -515,6 +531,17 @@ __global__ __launch_bounds__(XWG, 4) void rs_forney32_k(const RsDevTables *__res
         const uint32_t degmax = wave_max_full(deg);
         uint32_t magp[RS_NR / 4] = {0, 0, 0, 0, 0, 0, 0, 0};
         uint32_t fixed = 0;
+        /* the sums split at m = H, H = 8, 12 or 16 by the wave's degree
+         * (Omega_m for m < deg <= 2H, Lambda_(2h+1) for h < H): the upper
+         * halves' logs picked once, the chains run H steps */
+        const uint32_t H = degmax <= 16u ? 8u : degmax <= 24u ? 12u : 16u;
+        uint32_t oph[RS_NR / 2], ldh[RS_NR / 4];
+#pragma unroll
+        for (int b = 0; b < RS_NR / 2; ++b)
+            oph[b] = H == 8u ? opu[b + 8] : H == 12u ? opu[b + 12 < RS_NR ? b + 12 : RS_NR - 1] : opu[b + 16];
+#pragma unroll
+        for (int h = 0; h < RS_NR / 4; ++h)
+            ldh[h] = H == 8u ? lod[h + 4] : H == 12u ? lod[h + 6] : lod[h + 8];
 #pragma unroll
         for (int n0 = 0; n0 < RS_NR; n0 += XR) {
             if ((uint32_t)n0 >= degmax) /* uniform */
@@ -528,15 +555,17 @@ __global__ __launch_bounds__(XWG, 4) void rs_forney32_k(const RsDevTables *__res
             }
 #pragma unroll
             for (int b = 0; b < RS_NR / 2; ++b) {
+                if ((uint32_t)b < H) { /* uniform */
 #pragma unroll
-                for (int t = 0; t < XR; ++t) {
-                    num[t] ^= gf.expa(opu[b] + s[t]);
-                    nh[t] ^= gf.expa(opu[b + 16] + s[t]);
-                    if ((b & 1) == 0) {
-                        den[t] ^= gf.expa(lod[b >> 1] + s[t]);
-                        dh[t] ^= gf.expa(lod[(b >> 1) + 8] + s[t]);
+                    for (int t = 0; t < XR; ++t) {
+                        num[t] ^= gf.expa(opu[b] + s[t]);
+                        nh[t] ^= gf.expa(oph[b] + s[t]);
+                        if ((b & 1) == 0) {
+                            den[t] ^= gf.expa(lod[b >> 1] + s[t]);
+                            dh[t] ^= gf.expa(ldh[b >> 1] + s[t]);
+                        }
+                        s[t] = addmod7(s[t], si[t]);
                     }
-                    s[t] = addmod7(s[t], si[t]);
                 }
                 if (b & 1) {
 #pragma unroll
@@ -546,7 +575,7 @@ __global__ __launch_bounds__(XWG, 4) void rs_forney32_k(const RsDevTables *__res
                 }
             }
 #pragma unroll
-            for (int t = 0; t < XR; ++t) { /* s = 128 (16 i mod 255) */
+            for (int t = 0; t < XR; ++t) { /* s = 128 (H i mod 255) */
                 num[t] ^= gf.expa(gf.loga(nh[t]) + s[t]);
                 den[t] ^= gf.expa(gf.loga(dh[t]) + s[t]);
                 const uint32_t ln2 = mod255((uint32_t)((int32_t)ir[t] * ((int32_t)P.fcr - 1) + (int32_t)RS_NN));
