@@ -26,8 +26,9 @@
  * the reference's failure (:143-145) and finishes here.  Results are
  * bit-exact either way.
  *
- * Arrays are full length (Lambda_0..32, B_0..32), so BM needs ~100 VGPRs:
- * 4 waves/SIMD, one 1024-thread workgroup per CU.
+ * Arrays are full length (Lambda_0..32, B_0..32), so BM needs ~120 VGPRs:
+ * 4 waves/SIMD, one 1024-thread workgroup per CU.  Ablations (round 3,
+ * 16 erasures + 8 errors): BM ~60 % of rs_ebm_k, Omega ~13 %.
  */
 #include <hip/hip_runtime.h>
 
@@ -51,9 +52,12 @@ static int errata_grid(size_t count, int num_cu)
 /* ------------------------------------------------------------------------ */
 
 /*
- * Address-form logs as rs_bm_k (rs_fast.hip header).  The erasure locator
- * is built factor by factor, Lambda_j += X_l Lambda_(j-1) top down (three
- * lookups per coefficient); lanes past their count multiply by zero.  BM
+ * Address-form logs as rs_bm_k (rs_fast.hip header), Lambda kept as values:
+ * an update Lambda_j += q B_(j-1) is one lookup (B is kept in logs) and the
+ * logs of Lambda are taken once per iteration, for the discrepancy and B's
+ * copy.  The erasure locator is built factor by factor, Lambda_j += X_l
+ * Lambda_(j-1) top down (two lookups per coefficient); lanes past their
+ * count multiply by zero.  BM
  * then runs from the wave's smallest count: a lane is active from r = its
  * count + 1 (before that its Lambda and B stay as they are).  Massey's
  * unnormalised form with B = the erasure locator and b = 1 at the start, as
@@ -119,11 +123,14 @@ __global__ __launch_bounds__(XWG, 4) void rs_ebm_k(const RsDevTables *__restrict
             ne = 0;
 
         /* ---- erasure locator, src/decode.c:31-47 ---- */
-        uint32_t al[XL];
-        al[0] = pofs;
+        /* lv: Lambda_0..32 as values (Lambda_0 = 1 is never updated); a
+         * product term needs the log of the old coefficient only, so an
+         * update is two lookups (log, exp) and an XOR */
+        uint32_t lv[XL];
+        lv[0] = 1u;
 #pragma unroll
         for (int i = 1; i < XL; ++i)
-            al[i] = AZ;
+            lv[i] = 0u;
         const uint32_t nemax = wave_max_full(ne);
         {
             uint32_t q[RS_NR / 4]; /* slots shifted down one byte per factor */
@@ -145,7 +152,7 @@ __global__ __launch_bounds__(XWG, 4) void rs_ebm_k(const RsDevTables *__restrict
                     if ((uint32_t)(g - 3) <= l + 1u) { /* uniform */
 #pragma unroll
                         for (int j = g; j > g - 4 && j >= 1; --j)
-                            al[j] = gf.loga(gf.expa(al[j]) ^ gf.expa(al[j - 1] + xs));
+                            lv[j] ^= gf.expa((j == 1 ? pofs : gf.loga(lv[j - 1])) + xs);
                     }
                 }
             }
@@ -153,9 +160,16 @@ __global__ __launch_bounds__(XWG, 4) void rs_ebm_k(const RsDevTables *__restrict
 
         /* ---- Berlekamp-Massey, src/decode.c:49-96 ---- */
         uint32_t BP[(XL + 1) / 2]; /* B_0..B_33 address-form, two per register (B_33 stays zero) */
+        {
+            uint32_t gl[XL];
+            gl[0] = pofs;
 #pragma unroll
-        for (int k = 0; k < (XL + 1) / 2; ++k)
-            BP[k] = al[2 * k] | ((2 * k + 1 < XL ? al[2 * k + 1] : AZ) << 16);
+            for (int i = 1; i < XL; ++i)
+                gl[i] = (uint32_t)i <= nemax ? gf.loga(lv[i]) : AZ; /* Gamma has degree <= nemax */
+#pragma unroll
+            for (int k = 0; k < (XL + 1) / 2; ++k)
+                BP[k] = gl[2 * k] | ((2 * k + 1 < XL ? gl[2 * k + 1] : AZ) << 16);
+        }
         uint32_t dl = ne, db = ne, L = ne, lb = 0;
         const uint32_t nemin = 63u - wave_max_full(63u - (elig ? ne : 63u));
         uint32_t WL[18];
@@ -166,13 +180,30 @@ __global__ __launch_bounds__(XWG, 4) void rs_ebm_k(const RsDevTables *__restrict
             constexpr int s = decltype(sc)::value;
             const bool act = elig && r > ne;
             const uint32_t ub = wave_max_full(act ? dl : 0u);
-            uint32_t disc = 0;
+            /* logs of the old coefficients: the discrepancy's terms and B's copy;
+             * AZ above the wave's degree bound (those coefficients are zero) */
+            uint32_t la[XL];
+            la[0] = pofs;
 #pragma unroll
-            for (int g = 0; g < XL; g += 8) {
+            for (int g = 0; g < XL; g += 4) {
+#pragma unroll
+                for (int i = g; i < g + 4 && i < XL; ++i)
+                    if (i > 0)
+                        la[i] = AZ;
                 if ((uint32_t)g <= ub) {
 #pragma unroll
-                    for (int i = g; i < g + 8 && i < XL; ++i)
-                        disc ^= gf.expa(al[i] + half(WL, 3 - s + i)); /* S_(r-1-i) */
+                    for (int i = g; i < g + 4 && i < XL; ++i)
+                        if (i > 0)
+                            la[i] = gf.loga(lv[i]);
+                }
+            }
+            uint32_t disc = 0;
+#pragma unroll
+            for (int g = 0; g < XL; g += 4) {
+                if ((uint32_t)g <= ub) {
+#pragma unroll
+                    for (int i = g; i < g + 4 && i < XL; ++i)
+                        disc ^= gf.expa(la[i] + half(WL, 3 - s + i)); /* S_(r-1-i) */
                 }
             }
             const uint32_t ld = gf.logs(disc);
@@ -185,21 +216,18 @@ __global__ __launch_bounds__(XWG, 4) void rs_ebm_k(const RsDevTables *__restrict
 #pragma unroll
             for (int m = (XL - 1) / 4; m >= 0; --m) {
                 if ((uint32_t)(4 * m) <= ub2) {
-                    uint32_t old[4];
 #pragma unroll
                     for (int i = 4 * m + 3; i >= 4 * m; --i) {
-                        if (i >= XL)
+                        if (i >= XL || i == 0)
                             continue;
-                        old[i - 4 * m] = al[i];
-                        if (i > 0)
-                            al[i] = gf.loga(gf.expa(al[i]) ^ gf.expa(dq + half(BP, i - 1)));
+                        lv[i] ^= gf.expa(dq + half(BP, i - 1));
                     }
 #pragma unroll
                     for (int k = 2 * m + 1; k >= 2 * m; --k) {
                         if (k >= (XL + 1) / 2)
                             continue;
-                        const uint32_t lo = old[2 * k - 4 * m];
-                        const uint32_t hi = 2 * k + 1 < XL ? old[2 * k + 1 - 4 * m] : AZ;
+                        const uint32_t lo = la[2 * k];
+                        const uint32_t hi = 2 * k + 1 < XL ? la[2 * k + 1] : AZ;
                         const uint32_t sh = k > 0 ? __builtin_amdgcn_alignbyte(BP[k], BP[k - 1], 2)
                                                   : ((BP[0] << 16) | AZ);
                         BP[k] = lengthen ? (lo | (hi << 16)) : (act ? sh : BP[k]);
@@ -241,12 +269,18 @@ __global__ __launch_bounds__(XWG, 4) void rs_ebm_k(const RsDevTables *__restrict
         uint32_t deg = 0;
 #pragma unroll
         for (int i = 0; i < XL; ++i)
-            deg = (al[i] & 1u) ? (uint32_t)i : deg;
+            deg = lv[i] != 0u ? (uint32_t)i : deg;
         const bool fast = elig && deg == L && deg != 0u;
         if (elig && !fast) {
             meta[cw] = (uint8_t)(RS_ST_LIST << 5);
             list[atomicAdd(nlist, 1u)] = (uint32_t)cw;
         }
+        const uint32_t dmx = wave_max_full(fast ? deg : 0u);
+        uint32_t al[XL]; /* address-form logs of the final Lambda */
+        al[0] = pofs;
+#pragma unroll
+        for (int i = 1; i < XL; ++i)
+            al[i] = (uint32_t)i <= dmx ? gf.loga(lv[i]) : AZ;
 
         /* ---- Omega = S * Lambda mod x^deg (log form), src/decode.c:147-158 ---- */
         uint32_t ob[RS_NR / 4];
