@@ -299,12 +299,22 @@ __global__ __launch_bounds__(BWG, BM_WAVES) void rs_bm_k(const RsDevTables *__re
  * coefficient points at the all-zero rows e = 255 and steps by 255 * 256,
  * which the reduction maps back onto itself (no read leaves the table).
  */
+/* Chien point i' of flag bit b of word w (list entry 32 w + b): the flags
+ * of points 16h + 4d + b' sit at bit 8b' + 7 - d - 4h, so i' = 32 w + 28 -
+ * 4 (b & 7) + (b >> 3); entry 248 (bit 24 of word 7, masked as the repeat
+ * of i' = 0) stands for i = 255 */
+__device__ __forceinline__ uint32_t root_point(uint32_t e)
+{
+    return (e & 0xE0u) + 28u + ((e >> 3) & 3u) - 4u * (e & 7u);
+}
+
 __global__ __launch_bounds__(FWG, 8) void rs_chien_k(const RsDevTables *__restrict__ T, RsCorrParams P, size_t count,
                                                       const uint8_t *__restrict__ lam, uint8_t *__restrict__ meta,
                                                       uint8_t *__restrict__ roots, uint8_t *__restrict__ ok,
                                                       uint8_t *__restrict__ corrected)
 {
     __shared__ uint4 lch[256 * 16];
+    __shared__ uint4 lroot[FWG]; /* each lane's root list (64 + 16 KiB: two workgroups fill the 160 KiB) */
     {
         constexpr int K = 256 * 16 / FWG; /* every load first, then the stores */
         uint4 v[K];
@@ -357,17 +367,17 @@ __global__ __launch_bounds__(FWG, 8) void rs_chien_k(const RsDevTables *__restri
             A[k] = cb + (e << 8) + (jm << 4);
             inc[k] = e == 255u ? WRAP : (jm == 15u ? 256u : (jm + 1u) << 12);
         }
-        /* the roots as a byte list (src/decode.c:117-141 order: i' = 1..254,
-         * then i = 255), pushed in at byte 0 as they are found (newest
-         * first); Forney reads them by compile-time index instead of walking
-         * a bitmap (the walk cost rs_forney_k 38 of its 97 us) */
-        uint32_t L[4] = {0, 0, 0, 0};
+        /* the roots as a byte list in the lane's 16 LDS bytes, one ds_write_b8
+         * per root (a register shift list cost ~30 % of the kernel's VALU in
+         * the divergent loop); Forney reads them by compile-time index
+         * instead of walking a bitmap (the walk cost rs_forney_k 38 of its
+         * 97 us).  Entries are flag-bit indices 32 w + b (root_point()). */
+        lroot[threadIdx.x] = make_uint4(0, 0, 0, 0);
+        uint32_t lp = lds_addr(lroot) + 16u * threadIdx.x;
         uint32_t cnt = 0, z0 = 0;
         auto push = [&](uint32_t v) __attribute__((always_inline)) {
-            L[3] = __builtin_amdgcn_alignbyte(L[3], L[2], 3);
-            L[2] = __builtin_amdgcn_alignbyte(L[2], L[1], 3);
-            L[1] = __builtin_amdgcn_alignbyte(L[1], L[0], 3);
-            L[0] = (L[0] << 8) | v;
+            lds_st8(lp, v);
+            lp += 1u;
         };
 #pragma unroll 1
         for (int w = 0; w < 8; ++w) {
@@ -400,23 +410,25 @@ __global__ __launch_bounds__(FWG, 8) void rs_chien_k(const RsDevTables *__restri
                 word &= ~0x80u;
             }
             cnt += __popc(word);
-            const uint32_t wb = 32u * (uint32_t)w + 28u;
+            const uint32_t wb = 32u * (uint32_t)w;
             while (word != 0u) { /* at most deg <= 16 pushes per lane in all */
                 const uint32_t b = __builtin_ctz(word);
                 word &= word - 1u;
-                push(wb + (b >> 3) - 4u * (b & 7u)); /* bit 8b' + k: point 28 - 4k + b' */
+                push(wb | b);
             }
         }
         if (z0)
-            push(255u);
+            push(248u); /* flag bit 24 of word 7: root_point() = 255 */
         cnt += z0;
+        const uint4 l4r = lroot[threadIdx.x];
+        const uint32_t L[4] = {l4r.x, l4r.y, l4r.z, l4r.w};
         bool good = cnt == deg; /* src/decode.c:143-145 */
         if (P.pad > 0) {
             /* locations k = (i iprim - 1) mod 255 below pad fail, src/decode.c:132-134 */
             bool low = false;
 #pragma unroll
             for (int n = 0; n < 16; ++n) {
-                const uint32_t i = (L[n >> 2] >> (8 * (n & 3))) & 0xffu;
+                const uint32_t i = root_point((L[n >> 2] >> (8 * (n & 3))) & 0xffu);
                 low |= (uint32_t)n < cnt && (int32_t)((i * P.iprim + 254u) % 255u) < P.pad;
             }
             good = good && !low;
@@ -512,8 +524,8 @@ __global__ __launch_bounds__(FWG, FORNEY_WAVES) void rs_forney_k(const RsDevTabl
                 continue;
             uint32_t ir[FORNEY_R];
 #pragma unroll
-            for (int t = 0; t < FORNEY_R; ++t)
-                ir[t] = (rl[(n + t) >> 2] >> (8 * ((n + t) & 3))) & 0xffu; /* any order: roots are independent */
+            for (int t = 0; t < FORNEY_R; ++t) /* any order: roots are independent */
+                ir[t] = root_point((rl[(n + t) >> 2] >> (8 * ((n + t) & 3))) & 0xffu);
             /* powers alpha^(i m) as plain scaled logs 128 (i m mod 255), even
              * and odd m in two chains */
             uint32_t i2[FORNEY_R], ie[FORNEY_R], io[FORNEY_R], nm[FORNEY_R], den[FORNEY_R];

@@ -27,6 +27,10 @@ typedef __attribute__((address_space(3))) const lds_u32x4_t lds_u32x4;
 __device__ __forceinline__ uint32_t lds8(uint32_t a) { return *(lds_u8 *)(size_t)a; }
 __device__ __forceinline__ uint32_t lds16(uint32_t a) { return *(lds_u16 *)(size_t)a; }
 __device__ __forceinline__ lds_u32x4_t lds128(uint32_t a) { return *(lds_u32x4 *)(size_t)a; }
+__device__ __forceinline__ void lds_st8(uint32_t a, uint32_t v)
+{
+    *(__attribute__((address_space(3))) uint8_t *)(size_t)a = (uint8_t)v;
+}
 /* LDS byte address of a __shared__ object (also makes the object escape,
  * so its stores are never dropped as unread) */
 template <typename T> __device__ __forceinline__ uint32_t lds_addr(const T *p)
