@@ -30,7 +30,7 @@ under a launcher (WORLD_SIZE set, which must equal N).  One process per GPU,
 RCCL (`nccl` backend) only for barriers and the max-time / checksum
 reductions; no data-path collective.
 
-Also reported: per-kernel HIP-event times (in-library, on the launch stream),
+Also reported: per-kernel HIP-event times (in-library, stamped by each kernel's dispatch),
 the roofline of the dominant kernel, erasure decode (configs[3]), the
 host-memory pipeline (PCIe-inclusive), single-codeword call latency, and the
 reference CPU path timed on the host cores (rank 0, N=1 only).
@@ -131,7 +131,7 @@ def load_traffic(path):
 
 def path_roofline(mode, kt, steps, B, traffic):
     """Path-level roofline of one mode: 255 B x codewords per step / the sum of
-    the mode's kernel times per step (HIP events on the launch stream)."""
+    the mode's kernel times per step (HIP events stamped by the kernels' dispatches on the launch stream)."""
     ks = [k for k in PATHS[mode] if k in kt and kt[k][1]]
     ms = sum(kt[k][0] / steps for k in ks)
     if ms <= 0:
@@ -423,9 +423,11 @@ def run_weak(be, ranks, args, rank, world):
         step(args.warmup + k)
     ranks.barrier(be.sync)
     elapsed = ranks.max(time.perf_counter() - t0)
-    # timed loop 2: the same steps on fresh copies with a HIP event pair around
-    # every launch (poporon_amd_timing) -- per-kernel times and the roofline;
-    # the events themselves cost ~9 % of a step, so they stay out of loop 1
+    # timed loop 2: the same steps on fresh copies with HIP events on every
+    # launch (poporon_amd_timing: hipExtLaunchKernel stamps them at the
+    # kernel's own start and end, so they agree with a rocprofv3 kernel trace)
+    # -- per-kernel times and the roofline; the events cost ~5 % of a step,
+    # so they stay out of loop 1
     kt = None
     elapsed_ev = None
     if be.kind == "gpu" and copies:
@@ -744,8 +746,8 @@ def main(argv=None):
         "hbm_frac_of_peak": round(value * CW_BYTES / 1e9 / (HBM_PEAK_GBS * world), 4),
         "step": f"encode {B} messages + decode {B} corrupted codewords (16 errors each); the test channel corrupts "
                 "one copy per step before the timed loops; `value` / `ms_per_step` from a loop without per-kernel "
-                "events, per-kernel times and the roofline from a second loop of the same steps with a HIP event "
-                "pair around every launch (`ms_per_step_instrumented`)" if w["copies"]
+                "events, per-kernel times and the roofline from a second loop of the same steps with HIP events "
+                "stamped by every kernel's dispatch (`ms_per_step_instrumented`)" if w["copies"]
                 else "encode + channel (in place) + decode",
         "verified": w["nbad"] == 0,
         "weak_checksum": w["checksum"],
@@ -789,7 +791,7 @@ def main(argv=None):
         roof = dict(modes["decode16"])
         roof.update({"kernel": "decode16 path (" + " + ".join(P.KERNEL_NAMES[k] for k in roof["kernels_ms"]) + ")",
                      "note": "path-level: 255 B x codewords / sum of the path's kernel times per step (HIP events "
-                             "on the launch stream); traffic = HBM bytes of the same path from rocprofv3 "
+                             "stamped by each kernel's dispatch, hipExtLaunchKernel); traffic = HBM bytes of the same path from rocprofv3 "
                              "FETCH_SIZE x 2 + WRITE_SIZE (tools/pmc_traffic.py); the kernels are VALU/LDS-bound, "
                              "see DESIGN.md"})
         roof["kernels_ms"] = {P.KERNEL_NAMES[k]: v for k, v in roof["kernels_ms"].items()}

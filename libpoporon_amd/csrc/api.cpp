@@ -988,27 +988,39 @@ static hipEvent_t take_event(GpuCtx &g)
     return e;
 }
 
-/* Bracket one launch with events when timing is on. */
+/* Time the launches of one stage when timing is on: the events ride on the
+ * kernels' own dispatches (RS_LAUNCH, rs_device.h) */
+thread_local RsLaunchTimer rs_launch_timer = {nullptr, nullptr, 0};
+
 struct KernelTimer {
     GpuCtx &g;
     int kernel;
-    hipStream_t s;
     hipEvent_t a = nullptr, b = nullptr;
-    KernelTimer(GpuCtx &g_, int k, hipStream_t s_) : g(g_), kernel(k), s(s_)
+    KernelTimer(GpuCtx &g_, int k, hipStream_t) : g(g_), kernel(k)
     {
-        if (g.timing && (a = take_event(g)) != nullptr)
-            (void)hipEventRecord(a, s);
+        if (!g.timing || (a = take_event(g)) == nullptr)
+            return;
+        if ((b = take_event(g)) == nullptr) {
+            g.event_pool.push_back(a);
+            a = nullptr;
+            return;
+        }
+        rs_launch_timer = {a, b, 0};
     }
     void done()
     {
         if (!a)
             return;
-        if ((b = take_event(g)) != nullptr && hipEventRecord(b, s) == hipSuccess)
+        if (rs_launch_timer.n > 0) {
             g.pending.push_back({kernel, a, b});
-        else
+        } else { /* nothing launched */
             g.event_pool.push_back(a);
-        a = nullptr;
+            g.event_pool.push_back(b);
+        }
+        rs_launch_timer = {nullptr, nullptr, 0};
+        a = b = nullptr;
     }
+    ~KernelTimer() { done(); }
 };
 
 static bool drain_timing(GpuCtx &g)

@@ -21,6 +21,7 @@
 #include <algorithm>
 
 #include "bch_device.h"
+#include "rs_device.h" /* RS_LAUNCH */
 
 #define B_WG 256
 #define B_POLY 64 /* BCH_MAX_POLY, src/bch.c:12 */
@@ -226,7 +227,7 @@ extern "C" hipError_t bchk_encode(const BchParams *prm, const uint8_t *data, siz
 {
     if (count == 0)
         return hipSuccess;
-    hipLaunchKernelGGL(bch_encode_k, bch_grid(count, num_cu), dim3(B_WG), 0, stream, *prm, data, dstride, parity,
+    RS_LAUNCH(bch_encode_k, bch_grid(count, num_cu), dim3(B_WG), 0, stream, *prm, data, dstride, parity,
                        pstride, count);
     return hipGetLastError();
 }
@@ -237,7 +238,7 @@ extern "C" hipError_t bchk_decode(const BchParams *prm, uint8_t *data, size_t ds
 {
     if (count == 0)
         return hipSuccess;
-    hipLaunchKernelGGL(bch_decode_k, bch_grid(count, num_cu), dim3(B_WG), 0, stream, *prm, data, dstride, parity,
+    RS_LAUNCH(bch_decode_k, bch_grid(count, num_cu), dim3(B_WG), 0, stream, *prm, data, dstride, parity,
                        pstride, count, ok, corrected);
     return hipGetLastError();
 }

@@ -21,6 +21,7 @@
 #include <vector>
 
 #include "poporon/rng.h"
+#include "rs_device.h" /* RS_LAUNCH */
 
 #define EXPORT extern "C" __attribute__((visibility("default")))
 #define RNG_BLOCK 1024u /* words per lane */
@@ -226,7 +227,7 @@ extern "C" __attribute__((visibility("default"))) bool poporon_amd_rng_fill_devi
         return false;
     if (hipStreamSynchronize((hipStream_t)stream) != hipSuccess)
         return false;
-    hipLaunchKernelGGL(rng_fill_k, dim3((uint32_t)((nblocks + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+    RS_LAUNCH(rng_fill_k, dim3((uint32_t)((nblocks + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
                        r->d_starts, (uint8_t *)d_dest, size, nblocks);
     if (hipGetLastError() != hipSuccess)
         return false;

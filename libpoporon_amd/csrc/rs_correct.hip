@@ -813,14 +813,17 @@ extern "C" hipError_t rsk_correct(const RsDevTables *tab, const RsCorrParams *pr
         return hipSuccess;
     const dim3 grid(persistent_grid(count, COR_WG, num_cu));
     if (pos32)
-        hipLaunchKernelGGL((rs_correct_k<uint32_t, true>), grid, dim3(COR_WG), 0, stream, tab, *prm, data, dstride,
-                           parity, pstride, count, syn, syn16, syn16_stride, pos32, pos_stride, cnt, ok, corrected, nullptr, nullptr);
+        RS_LAUNCH((rs_correct_k<uint32_t, true>), grid, dim3(COR_WG), 0, stream, tab, *prm, data, dstride,
+                           parity, pstride, count, syn, syn16, syn16_stride, pos32, pos_stride, cnt, ok, corrected, nullptr, nullptr, nullptr,
+                  nullptr);
     else if (pos8)
-        hipLaunchKernelGGL((rs_correct_k<uint8_t, true>), grid, dim3(COR_WG), 0, stream, tab, *prm, data, dstride,
-                           parity, pstride, count, syn, syn16, syn16_stride, pos8, pos_stride, cnt, ok, corrected, nullptr, nullptr);
+        RS_LAUNCH((rs_correct_k<uint8_t, true>), grid, dim3(COR_WG), 0, stream, tab, *prm, data, dstride,
+                           parity, pstride, count, syn, syn16, syn16_stride, pos8, pos_stride, cnt, ok, corrected, nullptr, nullptr, nullptr,
+                  nullptr);
     else /* error mode */
-        hipLaunchKernelGGL((rs_correct_k<uint8_t, false>), grid, dim3(COR_WG), 0, stream, tab, *prm, data, dstride,
-                           parity, pstride, count, syn, syn16, syn16_stride, pos8, pos_stride, cnt, ok, corrected, nullptr, nullptr);
+        RS_LAUNCH((rs_correct_k<uint8_t, false>), grid, dim3(COR_WG), 0, stream, tab, *prm, data, dstride,
+                           parity, pstride, count, syn, syn16, syn16_stride, pos8, pos_stride, cnt, ok, corrected, nullptr, nullptr, nullptr,
+                  nullptr);
     return hipGetLastError();
 }
 
@@ -836,8 +839,8 @@ extern "C" hipError_t rsk_correct_list(const RsDevTables *tab, const RsCorrParam
     /* full persistent grid: the list is empty for codewords with at most 16
      * errors, and blocks past its length leave before filling their tables */
     const dim3 grid(persistent_grid(count, COR_WG, num_cu));
-    hipLaunchKernelGGL((rs_correct_k<uint8_t, false>), grid, dim3(COR_WG), 0, stream, tab, *prm, data, dstride,
-                       parity, pstride, count, syn, nullptr, 0, nullptr, 0, nullptr, ok, corrected, list, list_n);
+    RS_LAUNCH((rs_correct_k<uint8_t, false>), grid, dim3(COR_WG), 0, stream, tab, *prm, data, dstride,
+                       parity, pstride, count, syn, nullptr, 0, nullptr, 0, nullptr, ok, corrected, list, list_n, nullptr, nullptr);
     return hipGetLastError();
 }
 
@@ -852,11 +855,11 @@ extern "C" hipError_t rsk_correct_era_rec(const RsDevTables *tab, const RsCorrPa
         return hipSuccess;
     const dim3 grid(persistent_grid(count, COR_WG, num_cu));
     if (pos32)
-        hipLaunchKernelGGL((rs_correct_k<uint32_t, true, true>), grid, dim3(COR_WG), 0, stream, tab, *prm, nullptr,
+        RS_LAUNCH((rs_correct_k<uint32_t, true, true>), grid, dim3(COR_WG), 0, stream, tab, *prm, nullptr,
                            0, nullptr, 0, count, syn, nullptr, 0, pos32, pos_stride, cnt, ok, corrected, nullptr,
                            nullptr, rec, meta);
     else
-        hipLaunchKernelGGL((rs_correct_k<uint8_t, true, true>), grid, dim3(COR_WG), 0, stream, tab, *prm, nullptr, 0,
+        RS_LAUNCH((rs_correct_k<uint8_t, true, true>), grid, dim3(COR_WG), 0, stream, tab, *prm, nullptr, 0,
                            nullptr, 0, count, syn, nullptr, 0, pos8, pos_stride, cnt, ok, corrected, nullptr, nullptr,
                            rec, meta);
     return hipGetLastError();
@@ -873,7 +876,7 @@ extern "C" hipError_t rsk_correct_era_list(const RsDevTables *tab, const RsCorrP
         return hipSuccess;
     /* full persistent grid: blocks past the list's length leave at once */
     const dim3 grid(persistent_grid(count, COR_WG, num_cu));
-    hipLaunchKernelGGL((rs_correct_k<uint8_t, true, true>), grid, dim3(COR_WG), 0, stream, tab, *prm, nullptr, 0,
+    RS_LAUNCH((rs_correct_k<uint8_t, true, true>), grid, dim3(COR_WG), 0, stream, tab, *prm, nullptr, 0,
                        nullptr, 0, count, syn, nullptr, 0, pos8, pos_stride, cnt, ok, corrected, list, list_n, rec,
                        meta);
     return hipGetLastError();

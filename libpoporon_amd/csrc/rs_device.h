@@ -8,7 +8,28 @@
 #include <stddef.h>
 #include <stdint.h>
 
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
+
+/* Per-kernel timing (api.cpp KernelTimer): while set, every launch passes
+ * these events to hipExtLaunchKernel, which stamps them at the kernel's own
+ * start (first launch) and end (each launch; the last one stands), so a timed
+ * interval holds no queueing or event-record gaps and agrees with a
+ * rocprofv3 kernel trace.  Host-side, one per thread (the multi-GPU entry
+ * points run one thread per device). */
+struct RsLaunchTimer {
+    hipEvent_t start, stop;
+    int n;
+};
+extern thread_local RsLaunchTimer rs_launch_timer;
+#define RS_LAUNCH(K, G, B, SH, S, ...)                                                                    \
+    do {                                                                                                 \
+        if (rs_launch_timer.stop)                                                                        \
+            hipExtLaunchKernelGGL(K, G, B, SH, S, rs_launch_timer.n++ ? nullptr : rs_launch_timer.start, \
+                                  rs_launch_timer.stop, 0u, __VA_ARGS__);                                \
+        else                                                                                             \
+            hipLaunchKernelGGL(K, G, B, SH, S, __VA_ARGS__);                                             \
+    } while (0)
 
 #define RS_NR 32      /* num_roots served by the kernels */
 #define RS_A0 255u    /* log of zero */

@@ -667,7 +667,7 @@ extern "C" hipError_t rsk_ebm(const RsDevTables *tab, const RsCorrParams *prm, c
 {
     if (count == 0)
         return hipSuccess;
-    hipLaunchKernelGGL(rs_ebm_k, dim3(errata_grid(count, num_cu)), dim3(XWG), 0, stream, tab, *prm, ws->syn, pos8,
+    RS_LAUNCH(rs_ebm_k, dim3(errata_grid(count, num_cu)), dim3(XWG), 0, stream, tab, *prm, ws->syn, pos8,
                        pos_stride, cnt, count, ws->ext, ws->meta, ws->list, ws->nlist, ok, corrected, only_pend);
     return hipGetLastError();
 }
@@ -677,7 +677,7 @@ extern "C" hipError_t rsk_chien32(const RsDevTables *tab, const RsCorrParams *pr
 {
     if (count == 0)
         return hipSuccess;
-    hipLaunchKernelGGL(rs_chien32_k, dim3(errata_grid(count, num_cu)), dim3(XWG), 0, stream, tab, *prm, count,
+    RS_LAUNCH(rs_chien32_k, dim3(errata_grid(count, num_cu)), dim3(XWG), 0, stream, tab, *prm, count,
                        ws->ext, ws->meta, ws->roots, ok, corrected, only_pend ? ws->nlist + 1 : nullptr);
     return hipGetLastError();
 }
@@ -688,7 +688,7 @@ extern "C" hipError_t rsk_forney32(const RsDevTables *tab, const RsCorrParams *p
 {
     if (count == 0)
         return hipSuccess;
-    hipLaunchKernelGGL(rs_forney32_k, dim3(errata_grid(count, num_cu)), dim3(XWG), 0, stream, tab, *prm, pos8,
+    RS_LAUNCH(rs_forney32_k, dim3(errata_grid(count, num_cu)), dim3(XWG), 0, stream, tab, *prm, pos8,
                        pos_stride, count, ws->ext, ws->roots, ws->meta, ok, corrected, only_pend ? ws->nlist + 1 : nullptr);
     return hipGetLastError();
 }

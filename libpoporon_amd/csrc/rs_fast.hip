@@ -996,7 +996,7 @@ extern "C" hipError_t rsk_bm(const RsDevTables *tab, const RsSplitWs *ws, size_t
         return hipSuccess;
     const size_t need = (count + BWG - 1) / BWG,
                  res = FAST_ROUNDS * (size_t)(num_cu > 0 ? num_cu : 256) * (BM_WAVES * 256 / BWG);
-    hipLaunchKernelGGL(rs_bm_k, dim3((uint32_t)(need < res ? need : res)), dim3(BWG), 0, stream, tab, ws->syn, count,
+    RS_LAUNCH(rs_bm_k, dim3((uint32_t)(need < res ? need : res)), dim3(BWG), 0, stream, tab, ws->syn, count,
                        ws->lam,
                        ws->om, ws->meta, ws->list, ws->nlist, ok, corrected);
     return hipGetLastError();
@@ -1007,7 +1007,7 @@ extern "C" hipError_t rsk_chien(const RsDevTables *tab, const RsCorrParams *prm,
 {
     if (count == 0)
         return hipSuccess;
-    hipLaunchKernelGGL(rs_chien_k, dim3(fast_grid(count, num_cu)), dim3(FWG), 0, stream, tab, *prm, count, ws->lam,
+    RS_LAUNCH(rs_chien_k, dim3(fast_grid(count, num_cu)), dim3(FWG), 0, stream, tab, *prm, count, ws->lam,
                        ws->meta, ws->roots, ok, corrected);
     return hipGetLastError();
 }
@@ -1019,10 +1019,10 @@ extern "C" hipError_t rsk_forney(const RsDevTables *tab, const RsCorrParams *prm
     if (count == 0)
         return hipSuccess;
     if (prm->fcr == 1u && prm->iprim == 1u)
-        hipLaunchKernelGGL(rs_forney_k<true>, dim3(fast_grid(count, num_cu)), dim3(FWG), 0, stream, tab, *prm, data,
+        RS_LAUNCH(rs_forney_k<true>, dim3(fast_grid(count, num_cu)), dim3(FWG), 0, stream, tab, *prm, data,
                            dstride, parity, pstride, count, ws->lam, ws->om, ws->roots, ws->meta, ok, corrected);
     else
-        hipLaunchKernelGGL(rs_forney_k<false>, dim3(fast_grid(count, num_cu)), dim3(FWG), 0, stream, tab, *prm, data,
+        RS_LAUNCH(rs_forney_k<false>, dim3(fast_grid(count, num_cu)), dim3(FWG), 0, stream, tab, *prm, data,
                            dstride, parity, pstride, count, ws->lam, ws->om, ws->roots, ws->meta, ok, corrected);
     return hipGetLastError();
 }
@@ -1036,7 +1036,7 @@ static hipError_t apply_launch(const RsCorrParams *prm, const uint8_t *meta, con
     const uint32_t wire = prm->size == 223u && dstride == 255u && pstride == 255u && parity == data + 223 &&
                           (reinterpret_cast<uintptr_t>(data) & 15u) == 0u;
     const size_t waves = (count + 63) / 64;
-    hipLaunchKernelGGL(rs_apply_k<NC>, dim3((uint32_t)((waves + AWG / 64 - 1) / (AWG / 64))), dim3(AWG), 0, stream,
+    RS_LAUNCH(rs_apply_k<NC>, dim3((uint32_t)((waves + AWG / 64 - 1) / (AWG / 64))), dim3(AWG), 0, stream,
                        meta, rec, data, dstride, parity, pstride, prm->size, count, wire);
     return hipGetLastError();
 }
@@ -1061,7 +1061,7 @@ extern "C" hipError_t rsk_era(const RsDevTables *tab, const RsCorrParams *prm, c
         return hipSuccess;
     const size_t need = (count + EWG - 1) / EWG, /* persistent: more rounds measured slower for rs_era_k */
                  res = (size_t)(num_cu > 0 ? num_cu : 256) * (ERA_WAVES * 256 / EWG);
-    hipLaunchKernelGGL(rs_era_k, dim3((uint32_t)(need < res ? need : res)), dim3(EWG), 0, stream, tab, *prm, ws->syn, pos8,
+    RS_LAUNCH(rs_era_k, dim3((uint32_t)(need < res ? need : res)), dim3(EWG), 0, stream, tab, *prm, ws->syn, pos8,
                        pos_stride, cnt, count, ws->ext, ws->meta, ws->list, ws->nlist, ok, corrected, pend);
     return hipGetLastError();
 }

@@ -31,6 +31,7 @@
 #include <algorithm>
 
 #include "rs_generic.h"
+#include "rs_device.h" /* RS_LAUNCH */
 
 #define G_WG_MAX 256
 
@@ -433,7 +434,7 @@ extern "C" hipError_t rsg_encode(const RsGenTables *tab, const RsGenParams *prm,
     uint32_t wg;
     size_t lds;
     g_shape(*prm, 1, wg, lds);
-    hipLaunchKernelGGL(rsg_encode_k, g_grid(count, wg, num_cu, lds), dim3(wg), lds, stream, tab, *prm, data, dstride,
+    RS_LAUNCH(rsg_encode_k, g_grid(count, wg, num_cu, lds), dim3(wg), lds, stream, tab, *prm, data, dstride,
                        parity, pstride, count);
     return hipGetLastError();
 }
@@ -450,10 +451,10 @@ extern "C" hipError_t rsg_decode(const RsGenTables *tab, const RsGenParams *prm,
     g_shape(*prm, 7, wg, lds);
     const dim3 grid = g_grid(count, wg, num_cu, lds);
     if (pos32)
-        hipLaunchKernelGGL(rsg_decode_k<uint32_t>, grid, dim3(wg), lds, stream, tab, *prm, data, dstride, parity,
+        RS_LAUNCH(rsg_decode_k<uint32_t>, grid, dim3(wg), lds, stream, tab, *prm, data, dstride, parity,
                            pstride, count, ext, ext_stride, pos32, pos_stride, cnt, ok, corrected);
     else
-        hipLaunchKernelGGL(rsg_decode_k<uint8_t>, grid, dim3(wg), lds, stream, tab, *prm, data, dstride, parity,
+        RS_LAUNCH(rsg_decode_k<uint8_t>, grid, dim3(wg), lds, stream, tab, *prm, data, dstride, parity,
                            pstride, count, ext, ext_stride, pos8, pos_stride, cnt, ok, corrected);
     return hipGetLastError();
 }
@@ -467,7 +468,7 @@ extern "C" hipError_t rsg_check(const RsGenTables *tab, const RsGenParams *prm, 
     uint32_t wg;
     size_t lds;
     g_shape(*prm, 1, wg, lds);
-    hipLaunchKernelGGL(rsg_check_k, g_grid(count, wg, num_cu, lds), dim3(wg), lds, stream, tab, *prm, data, dstride,
+    RS_LAUNCH(rsg_check_k, g_grid(count, wg, num_cu, lds), dim3(wg), lds, stream, tab, *prm, data, dstride,
                        parity, pstride, count, dirty, syn, syn_stride);
     return hipGetLastError();
 }

@@ -518,13 +518,13 @@ static hipError_t launch_lfsr(const RsDevTables *tab, const uint8_t *data, size_
     const dim3 grid(persistent_grid(count, LFSR_WG, num_cu)), block(LFSR_WG);
     uint8_t *par = const_cast<uint8_t *>(parity);
     if (size != FULL_K)
-        hipLaunchKernelGGL((rs_lfsr_k<MODE, PATH_GENERIC>), grid, block, 0, stream, tab, data, dstride, par, pstride,
+        RS_LAUNCH((rs_lfsr_k<MODE, PATH_GENERIC>), grid, block, 0, stream, tab, data, dstride, par, pstride,
                            size, count, out, reset);
     else if (MODE != MODE_ENCODE && parity == data + FULL_K && pstride == dstride)
-        hipLaunchKernelGGL((rs_lfsr_k<MODE, PATH_CONTIG>), grid, block, 0, stream, tab, data, dstride, par, pstride,
+        RS_LAUNCH((rs_lfsr_k<MODE, PATH_CONTIG>), grid, block, 0, stream, tab, data, dstride, par, pstride,
                            size, count, out, reset);
     else
-        hipLaunchKernelGGL((rs_lfsr_k<MODE, PATH_SPLIT>), grid, block, 0, stream, tab, data, dstride, par, pstride,
+        RS_LAUNCH((rs_lfsr_k<MODE, PATH_SPLIT>), grid, block, 0, stream, tab, data, dstride, par, pstride,
                            size, count, out, reset);
     return hipGetLastError();
 }
@@ -578,7 +578,7 @@ extern "C" hipError_t rsk_syn_log(const RsDevTables *tab, const uint8_t *syn, si
     if (count == 0)
         return hipSuccess;
     const size_t blocks = (count + 255) / 256;
-    hipLaunchKernelGGL(rs_synlog_k, dim3((uint32_t)blocks), dim3(256), 0, stream, tab, syn, count, out, stride, flag);
+    RS_LAUNCH(rs_synlog_k, dim3((uint32_t)blocks), dim3(256), 0, stream, tab, syn, count, out, stride, flag);
     return hipGetLastError();
 }
 

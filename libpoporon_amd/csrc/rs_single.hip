@@ -553,7 +553,7 @@ finish:
 extern "C" hipError_t rsk_encode1(const RsDevTables *tab, const uint8_t *data, uint8_t *parity, uint32_t size,
                                   uint32_t *flag, uint32_t seq, hipStream_t stream)
 {
-    hipLaunchKernelGGL(rs_enc1_k, dim3(1), dim3(S1_WG), 0, stream, tab, data, parity, size, flag, seq);
+    RS_LAUNCH(rs_enc1_k, dim3(1), dim3(S1_WG), 0, stream, tab, data, parity, size, flag, seq);
     return hipGetLastError();
 }
 
@@ -562,7 +562,7 @@ extern "C" hipError_t rsk_decode1(const RsDevTables *tab, const RsCorrParams *pr
                                   uint32_t cnt_bytes, const uint16_t *ext, uint8_t *ok, uint8_t *corrected,
                                   uint32_t *flag, uint32_t seq, hipStream_t stream)
 {
-    hipLaunchKernelGGL(rs_dec1_k, dim3(1), dim3(S1_WG), 0, stream, tab, *prm, mode, data, parity, pos8, pos32, cnt,
+    RS_LAUNCH(rs_dec1_k, dim3(1), dim3(S1_WG), 0, stream, tab, *prm, mode, data, parity, pos8, pos32, cnt,
                        cnt_bytes, ext, ok, corrected, flag, seq);
     return hipGetLastError();
 }
