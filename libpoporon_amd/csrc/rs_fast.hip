@@ -1,9 +1,10 @@
 /*
- * rs_fast.hip -- RS(255,223) error-mode decode split into three kernels,
- * each small enough in LDS (<= 64 KiB) and registers (<= 64 VGPRs) for two
- * 1024-thread workgroups per CU: 8 waves per SIMD, twice the occupancy of
- * the single correction kernel (rs_correct.hip, 160 KiB + 128 VGPRs), whose
- * time was half waiting on LDS results.  One codeword per lane.
+ * rs_fast.hip -- RS(255,223) error-mode decode split into small kernels,
+ * each small enough in LDS (<= 64 KiB) for two workgroups per CU: Chien and
+ * Forney at 8 waves per SIMD (<= 64 VGPRs), Berlekamp-Massey at 4 with three
+ * lookups per term -- against the single correction kernel (rs_correct.hip,
+ * 160 KiB + 128 VGPRs), whose time was half waiting on LDS results.  One
+ * codeword per lane.
  *
  *   rs_bm_k      syndromes -> Berlekamp-Massey (src/decode.c:49-96) -> Lambda,
  *                degree (:98-110), Omega (:147-158)
@@ -56,8 +57,8 @@
 #define NL 17          /* Lambda_0..16 and B_0..16: t = 16 */
 #define FORNEY_R 1     /* roots per Forney step (more spill at 64 VGPRs) */
 #define FORNEY_WAVES 8
-#define BWG 1024 /* rs_bm_k: 8 waves/SIMD; 4 or 6 measured slower (profiles/r03_bm_experiments.log) */
-#define BM_WAVES 8
+#define BWG 512 /* rs_bm_k: 4 waves/SIMD, two workgroups per CU (profiles/r03_bm_value.log) */
+#define BM_WAVES 4
 
 /* Grids of up to 8 resident rounds: at 2^20 codewords every workgroup takes
  * one batch.  A persistent grid (one round, each workgroup looping) measured
@@ -84,10 +85,13 @@ static int fast_grid(size_t count, int num_cu)
  * x^16 nonzero, `bo`) would give Lambda a term past x^16, and lengthening
  * to L > 16 ends with deg != L -- all of these go to the list.
  *
- * Syndromes enter a window of 20 u16 entries (10 VGPRs), four per block of
- * four iterations: at block q the entry e holds 128 log S_(4q+3-e), so term
- * i of iteration r = 4q+1+s reads entry 3 - s + i at a compile-time place
- * (the four iterations are unrolled; blocks are a rolled loop).
+ * Syndromes enter a window of 20 entries, four per block of four
+ * iterations: at block q the entry e holds 128 log S_(4q+3-e), so term i of
+ * iteration r = 4q+1+s reads entry 3 - s + i at a compile-time place (the
+ * four iterations are unrolled; blocks are a rolled loop).  Lambda is kept
+ * as the addresses of its log entries (below): 0.147 -> 0.137 ms against the
+ * 4-lookup log form at 8 waves/SIMD; the same at 8, 6 or 5 waves spilled
+ * (profiles/r03_bm_value.log).
  */
 __global__ __launch_bounds__(BWG, BM_WAVES) void rs_bm_k(const RsDevTables *__restrict__ T, const uint8_t *__restrict__ syn,
                                                    size_t count, uint8_t *__restrict__ lamo, uint8_t *__restrict__ omo,
@@ -124,74 +128,79 @@ __global__ __launch_bounds__(BWG, BM_WAVES) void rs_bm_k(const RsDevTables *__re
         }
 
         /* ---- Berlekamp-Massey, src/decode.c:49-96 (error mode: r = 1..32) ---- */
-        /* al: address-form logs of Lambda_0..16 (Lambda_0 = 1, never updated);
-         * BP: B_0..B_17 the same way, packed two per register (B_17 stays zero) */
-        uint32_t al[NL], BP[(NL + 1) / 2];
-        al[0] = pofs;
+        /* ---- Berlekamp-Massey, src/decode.c:49-96 (error mode: r = 1..32) ----
+         * hl: Lambda_0..16 as the LDS addresses of their log entries,
+         * pofs + 1 + 128 Lambda_i (bits 7..14 hold the value, the replica
+         * offset sits below), so an update Lambda_i += q B_(i-1) is
+         * hl ^= exp << 7 (one lookup) and Lambda's logs are one ds_read_u16
+         * each, taken once per iteration for the discrepancy and B's copy: 3
+         * lookups per term instead of 4.  B (address-form logs) and the
+         * syndrome window one register per entry: no half-word extractions
+         * (103 VGPRs, 4 waves/SIMD) */
+        const uint32_t HZ = pofs + 1u; /* hl of a zero coefficient */
+        uint32_t hl[NL], B[NL + 1];
+        hl[0] = HZ + 128u;
 #pragma unroll
         for (int i = 1; i < NL; ++i)
-            al[i] = AZ;
-        BP[0] = pofs | (AZ << 16);
+            hl[i] = HZ;
+        B[0] = pofs;
 #pragma unroll
-        for (int k = 1; k < (NL + 1) / 2; ++k)
-            BP[k] = AZ | (AZ << 16);
+        for (int k = 1; k <= NL; ++k)
+            B[k] = AZ;
         uint32_t dl = 0, db = 0, L = 0, lb = 0, ubp = 0;
         uint32_t over = 0, bo = 0; /* 0 / 1 */
-        uint32_t WL[10];
+        uint32_t WL[20];
 #pragma unroll
-        for (int k = 0; k < 10; ++k)
-            WL[k] = SZ | (SZ << 16);
+        for (int k = 0; k < 20; ++k)
+            WL[k] = SZ;
         uint32_t snext = any ? sa.x : 0u; /* S_0..S_3 */
 
         auto step = [&](auto sc, uint32_t r) __attribute__((always_inline)) {
             constexpr int s = decltype(sc)::value;
-            const uint32_t ub = ubp; /* dl <= the previous iteration's bound */
+            const uint32_t ub = ubp;
+            uint32_t la[NL];
             uint32_t disc = 0;
+            la[0] = pofs;
 #pragma unroll
-            for (int g = 0; g < NL; g += 8) {
+            for (int g = 0; g < NL; g += 4) {
+#pragma unroll
+                for (int i = g; i < g + 4 && i < NL; ++i)
+                    if (i > 0)
+                        la[i] = AZ;
                 if ((uint32_t)g <= ub) {
 #pragma unroll
-                    for (int i = g; i < g + 8 && i < NL; ++i)
-                        disc ^= gf.expa(al[i] + half(WL, 3 - s + i)); /* S_(r-1-i), zero where r-1-i < 0 */
+                    for (int i = g; i < g + 4 && i < NL; ++i) {
+                        if (i > 0)
+                            la[i] = lds16(hl[i]);
+                        disc ^= gf.expa(la[i] + WL[3 - s + i]); /* S_(r-1-i), zero where r-1-i < 0 */
+                    }
                 }
             }
             const uint32_t ld = gf.logs(disc);
             const bool upd = disc != 0u;
             const bool lengthen = upd && (2u * L <= r - 1u);
             const int32_t dd = (int32_t)ld - (int32_t)lb;
-            const uint32_t dq = upd ? (uint32_t)(dd < 0 ? dd + 255 * 128 : dd) : DQZ; /* scaled log of disc / b */
-            const uint32_t b16 = half(BP, NL - 1) != AZ;
-            over |= upd ? (bo | b16) : 0u;    /* Lambda would get a term past x^16 */
-            bo = lengthen ? 0u : (bo | b16); /* B <- x B pushes B_16 past the cut */
+            const uint32_t dq = upd ? (uint32_t)(dd < 0 ? dd + 255 * 128 : dd) : DQZ;
+            const uint32_t b16 = B[NL - 1] != AZ;
+            over |= upd ? (bo | b16) : 0u;
+            bo = lengthen ? 0u : (bo | b16);
             const uint32_t up = min((uint32_t)(NL - 1), max(dl, db + 1u));
             const uint32_t ub2 = wave_max_full(up);
             ubp = ub2;
-            /* groups of four coefficients 4m..4m+3 (two B pairs), top down:
-             * Lambda_i += q B_(i-1); B <- Lambda (old) or x B, pair k from the
-             * old pairs k and k-1 */
 #pragma unroll
             for (int m = (NL - 1) / 4; m >= 0; --m) {
                 if ((uint32_t)(4 * m) <= ub2) {
-                    uint32_t old[4];
 #pragma unroll
                     for (int i = 4 * m + 3; i >= 4 * m; --i) {
-                        if (i >= NL)
+                        if (i >= NL + 1)
                             continue;
-                        old[i - 4 * m] = al[i];
-                        if (i > 0) {
-                            const uint32_t v = gf.expa(al[i]) ^ gf.expa(dq + half(BP, i - 1));
-                            al[i] = gf.loga(v);
+                        if (i > 0 && i < NL) {
+                            uint32_t e7;
+                            const uint32_t e = gf.expa(dq + B[i - 1]);
+                            asm("v_lshlrev_b16 %0, 7, %1" : "=v"(e7) : "v"(e));
+                            hl[i] ^= e7;
                         }
-                    }
-#pragma unroll
-                    for (int k = 2 * m + 1; k >= 2 * m; --k) {
-                        if (k >= (NL + 1) / 2)
-                            continue;
-                        const uint32_t lo = old[2 * k - 4 * m];
-                        const uint32_t hi = 2 * k + 1 < NL ? old[2 * k + 1 - 4 * m] : AZ;
-                        const uint32_t sh = k > 0 ? __builtin_amdgcn_alignbyte(BP[k], BP[k - 1], 2)
-                                                  : ((BP[0] << 16) | AZ);
-                        BP[k] = lengthen ? (lo | (hi << 16)) : sh;
+                        B[i] = lengthen ? (i < NL ? la[i] : AZ) : (i > 0 ? B[i - 1] : AZ);
                     }
                 }
             }
@@ -209,19 +218,23 @@ __global__ __launch_bounds__(BWG, BM_WAVES) void rs_bm_k(const RsDevTables *__re
             if (q + 1u < RS_NR / 4) /* uniform */
                 snext = any ? sp[q + 1u] : 0u;
             /* shift the window by four entries, S_(4q+3) .. S_(4q) in front */
-#pragma unroll
-            for (int k = 9; k >= 2; --k)
-                WL[k] = WL[k - 2];
             const uint32_t s0 = gf.logs(sd & 0xffu), s1 = gf.logs((sd >> 8) & 0xffu);
             const uint32_t s2 = gf.logs((sd >> 16) & 0xffu), s3 = gf.logs(sd >> 24);
-            WL[0] = s3 | (s2 << 16);
-            WL[1] = s1 | (s0 << 16);
+#pragma unroll
+            for (int k = 19; k >= 4; --k)
+                WL[k] = WL[k - 4];
+            WL[0] = s3, WL[1] = s2, WL[2] = s1, WL[3] = s0;
             step(std::integral_constant<int, 0>{}, 4u * q + 1u);
             step(std::integral_constant<int, 1>{}, 4u * q + 2u);
             step(std::integral_constant<int, 2>{}, 4u * q + 3u);
             step(std::integral_constant<int, 3>{}, 4u * q + 4u);
         }
 
+        uint32_t al[NL]; /* address-form logs of the final Lambda */
+        al[0] = pofs;
+#pragma unroll
+        for (int i = 1; i < NL; ++i)
+            al[i] = (uint32_t)i <= ubp ? lds16(hl[i]) : AZ;
         /* ---- degree, src/decode.c:98-110 ---- */
         uint32_t deg = 0;
 #pragma unroll
