@@ -52,10 +52,10 @@ static int errata_grid(size_t count, int num_cu)
 /* ------------------------------------------------------------------------ */
 
 /*
- * Address-form logs as rs_bm_k (rs_fast.hip header), Lambda kept as values:
- * an update Lambda_j += q B_(j-1) is one lookup (B is kept in logs) and the
- * logs of Lambda are taken once per iteration, for the discrepancy and B's
- * copy.  The erasure locator is built factor by factor, Lambda_j += X_l
+ * Address-form logs as rs_bm_k (rs_fast.hip header), Lambda kept as the
+ * addresses of its log entries (GfA::hz): an update Lambda_j += q B_(j-1) is
+ * one lookup (B is kept in logs) and the logs of Lambda are taken once per
+ * iteration (one ds_read_u16 each), for the discrepancy and B's copy.  The erasure locator is built factor by factor, Lambda_j += X_l
  * Lambda_(j-1) top down (two lookups per coefficient); lanes past their
  * count multiply by zero.  BM
  * then runs from the wave's smallest count: a lane is active from r = its
@@ -123,14 +123,15 @@ __global__ __launch_bounds__(XWG, 4) void rs_ebm_k(const RsDevTables *__restrict
             ne = 0;
 
         /* ---- erasure locator, src/decode.c:31-47 ---- */
-        /* lv: Lambda_0..32 as values (Lambda_0 = 1 is never updated); a
-         * product term needs the log of the old coefficient only, so an
-         * update is two lookups (log, exp) and an XOR */
+        /* lv: Lambda_0..32 as log-entry addresses (GfA::hz; Lambda_0 = 1 is
+         * never updated); a product term needs the log of the old
+         * coefficient only, so an update is two lookups (log, exp) */
+        const uint32_t HZ = gf.hz();
         uint32_t lv[XL];
-        lv[0] = 1u;
+        lv[0] = HZ + 128u;
 #pragma unroll
         for (int i = 1; i < XL; ++i)
-            lv[i] = 0u;
+            lv[i] = HZ;
         const uint32_t nemax = wave_max_full(ne);
         {
             uint32_t q[RS_NR / 4]; /* slots shifted down one byte per factor */
@@ -152,7 +153,7 @@ __global__ __launch_bounds__(XWG, 4) void rs_ebm_k(const RsDevTables *__restrict
                     if ((uint32_t)(g - 3) <= l + 1u) { /* uniform */
 #pragma unroll
                         for (int j = g; j > g - 4 && j >= 1; --j)
-                            lv[j] ^= gf.expa((j == 1 ? pofs : gf.loga(lv[j - 1])) + xs);
+                            lv[j] ^= shl7(gf.expa((j == 1 ? pofs : gf.logh(lv[j - 1])) + xs));
                     }
                 }
             }
@@ -165,7 +166,7 @@ __global__ __launch_bounds__(XWG, 4) void rs_ebm_k(const RsDevTables *__restrict
             gl[0] = pofs;
 #pragma unroll
             for (int i = 1; i < XL; ++i)
-                gl[i] = (uint32_t)i <= nemax ? gf.loga(lv[i]) : AZ; /* Gamma has degree <= nemax */
+                gl[i] = (uint32_t)i <= nemax ? gf.logh(lv[i]) : AZ; /* Gamma has degree <= nemax */
 #pragma unroll
             for (int k = 0; k < (XL + 1) / 2; ++k)
                 BP[k] = gl[2 * k] | ((2 * k + 1 < XL ? gl[2 * k + 1] : AZ) << 16);
@@ -194,7 +195,7 @@ __global__ __launch_bounds__(XWG, 4) void rs_ebm_k(const RsDevTables *__restrict
 #pragma unroll
                     for (int i = g; i < g + 4 && i < XL; ++i)
                         if (i > 0)
-                            la[i] = gf.loga(lv[i]);
+                            la[i] = gf.logh(lv[i]);
                 }
             }
             uint32_t disc = 0;
@@ -220,7 +221,7 @@ __global__ __launch_bounds__(XWG, 4) void rs_ebm_k(const RsDevTables *__restrict
                     for (int i = 4 * m + 3; i >= 4 * m; --i) {
                         if (i >= XL || i == 0)
                             continue;
-                        lv[i] ^= gf.expa(dq + half(BP, i - 1));
+                        lv[i] ^= shl7(gf.expa(dq + half(BP, i - 1)));
                     }
 #pragma unroll
                     for (int k = 2 * m + 1; k >= 2 * m; --k) {
@@ -269,7 +270,7 @@ __global__ __launch_bounds__(XWG, 4) void rs_ebm_k(const RsDevTables *__restrict
         uint32_t deg = 0;
 #pragma unroll
         for (int i = 0; i < XL; ++i)
-            deg = lv[i] != 0u ? (uint32_t)i : deg;
+            deg = lv[i] != HZ ? (uint32_t)i : deg;
         const bool fast = elig && deg == L && deg != 0u;
         if (elig && !fast) {
             meta[cw] = (uint8_t)(RS_ST_LIST << 5);
@@ -280,7 +281,7 @@ __global__ __launch_bounds__(XWG, 4) void rs_ebm_k(const RsDevTables *__restrict
         al[0] = pofs;
 #pragma unroll
         for (int i = 1; i < XL; ++i)
-            al[i] = (uint32_t)i <= dmx ? gf.loga(lv[i]) : AZ;
+            al[i] = (uint32_t)i <= dmx ? gf.logh(lv[i]) : AZ;
 
         /* ---- Omega = S * Lambda mod x^deg (log form), src/decode.c:147-158 ---- */
         uint32_t ob[RS_NR / 4];

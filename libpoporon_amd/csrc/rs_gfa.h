@@ -56,7 +56,21 @@ struct GfA {
     __device__ __forceinline__ uint32_t afrom(uint32_t b) const { return b < 255u ? (b << 7) + pofs : az(); }
     /* alpha^l of a plain log l < 255 */
     __device__ __forceinline__ uint32_t exp(uint32_t l) const { return lds8(pofs + (l << 7)); }
+    /* "log-entry address" form of a value v: pofs + 1 + 128 v, the address
+     * loga reads (bits 7..14 = v, the replica offset below: XOR of v << 7
+     * adds to v); its log is one ds_read_u16 */
+    __device__ __forceinline__ uint32_t hz() const { return pofs + 1u; }
+    __device__ __forceinline__ uint32_t logh(uint32_t h) const { return lds16(h); }
 };
+
+/* v << 7 for a byte v in one full-rate 16-bit op (VOP2 16-bit results zero
+ * bits 31:16 on gfx950) */
+__device__ __forceinline__ uint32_t shl7(uint32_t v)
+{
+    uint32_t r;
+    asm("v_lshlrev_b16 %0, 7, %1" : "=v"(r) : "v"(v));
+    return r;
+}
 
 /* compile-time loop: f(std::integral_constant<int, i>) for i = I, I+S, ... < E */
 template <int I, int E, int S, class F>
