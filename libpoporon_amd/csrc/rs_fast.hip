@@ -1,8 +1,8 @@
 /*
  * rs_fast.hip -- RS(255,223) error-mode decode split into small kernels,
- * each small enough in LDS (<= 64 KiB) for two workgroups per CU: Chien and
- * Forney at 8 waves per SIMD (<= 64 VGPRs), Berlekamp-Massey at 4 with three
- * lookups per term -- against the single correction kernel (rs_correct.hip,
+ * each small enough in LDS (<= 64 KiB) for two workgroups per CU: Chien at 8
+ * waves per SIMD (<= 64 VGPRs), Forney at 6 and Berlekamp-Massey at 4 with
+ * fewer instructions per term -- against the single correction kernel (rs_correct.hip,
  * 160 KiB + 128 VGPRs), whose time was half waiting on LDS results.  One
  * codeword per lane.
  *
@@ -55,8 +55,6 @@
 
 #define FWG 1024       /* threads per workgroup; two workgroups per CU */
 #define NL 17          /* Lambda_0..16 and B_0..16: t = 16 */
-#define FORNEY_R 1     /* roots per Forney step (more spill at 64 VGPRs) */
-#define FORNEY_WAVES 8
 #define BWG 512 /* rs_bm_k: 4 waves/SIMD, two workgroups per CU (profiles/r03_bm_value.log) */
 #define BM_WAVES 4
 
@@ -460,34 +458,40 @@ __global__ __launch_bounds__(FWG, 8) void rs_chien_k(const RsDevTables *__restri
 }
 
 /* ------------------------------------------------------------------------ */
-/* rs_forney_k: magnitudes and apply                                         */
+/* rs_forney_k: magnitudes                                                   */
 /* ------------------------------------------------------------------------ */
 
 /*
- * Per root i (ascending, src/decode.c:136-138): num = sum_m Omega_m
- * alpha^(i m), den = sum_(2h <= dtop) Lambda_(2h+1) alpha^(2h i), magnitude
- * alpha^(log num + log alpha^(i (fcr-1)) + 255 - log den) (no den = 0 guard,
- * as the reference); a zero numerator corrects nothing and is not counted.
- * FORNEY_R roots per step (their lookups issue together).  The locations and
- * magnitudes go out as a 32-byte record per codeword for rs_apply_k.
+ * Per root i (src/decode.c:136-138, any order: the roots are independent):
+ * num = sum_m Omega_m alpha^(i m), den = sum_(2h <= dtop) Lambda_(2h+1)
+ * alpha^(2h i), magnitude alpha^(log num + log alpha^(i (fcr-1)) + 255 -
+ * log den) (no den = 0 guard, as the reference); a zero numerator corrects
+ * nothing and is not counted.  The sums split at m = 8: one 8-step power
+ * chain per root serves Omega_0..7 / Omega_8..15 and the derivative's lower
+ * / upper four terms, merged by alpha^(8i); four roots per step, the logs
+ * unpacked (80 VGPRs, 6 waves/SIMD in 768-thread groups: 0.062 -> 0.059 ms
+ * against the even/odd chains at 8 waves, profiles/r03_forney_split8.log).
+ * The locations and magnitudes go out as a 32-byte record per codeword for
+ * rs_apply_k.
  */
-template <bool P11> /* fcr = 1 and prim = 1 (the default config): no multiplies for ln2 / locations */
-__global__ __launch_bounds__(FWG, FORNEY_WAVES) void rs_forney_k(const RsDevTables *__restrict__ T, RsCorrParams P,
-                                                       uint8_t *data, size_t dstride, uint8_t *parity, size_t pstride,
-                                                       size_t count, const uint8_t *__restrict__ lam,
-                                                       const uint8_t *__restrict__ om,
-                                                       uint8_t *__restrict__ roots,
-                                                       const uint8_t *__restrict__ meta, uint8_t *__restrict__ ok,
-                                                       uint8_t *__restrict__ corrected)
+#define F2WG 768 /* a multiple of four waves: 640-thread groups leave SIMDs uneven (0.084 ms) */
+template <bool P11>
+__global__ __launch_bounds__(F2WG, 6) void rs_forney_k(const RsDevTables *__restrict__ T, RsCorrParams P,
+                                                      uint8_t *data, size_t dstride, uint8_t *parity, size_t pstride,
+                                                      size_t count, const uint8_t *__restrict__ lam,
+                                                      const uint8_t *__restrict__ om, uint8_t *__restrict__ roots,
+                                                      const uint8_t *__restrict__ meta, uint8_t *__restrict__ ok,
+                                                      uint8_t *__restrict__ corrected)
 {
     __shared__ uint32_t lgf[512 * 32];
-    fill_gfa<FWG>(lgf, T);
+    fill_gfa<F2WG>(lgf, T);
     __syncthreads();
     const GfA gf{lds_addr(lgf) + 4u * (threadIdx.x & 31u) + 1u};
     const int32_t pad = P.pad;
     constexpr bool fcr1 = P11, iprim1 = P11;
+    constexpr int R = 4;
 
-    for (size_t base = (size_t)blockIdx.x * FWG; base < count; base += (size_t)gridDim.x * FWG) {
+    for (size_t base = (size_t)blockIdx.x * F2WG; base < count; base += (size_t)gridDim.x * F2WG) {
         const size_t cw = base + threadIdx.x;
         const bool valid = cw < count;
         const uint32_t st = valid ? meta[cw] : 0u;
@@ -496,7 +500,7 @@ __global__ __launch_bounds__(FWG, FORNEY_WAVES) void rs_forney_k(const RsDevTabl
             continue;
         const uint32_t deg = fast ? (st & 31u) : 0u;
         uint4 o4 = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu), l4 = o4;
-        uint32_t rl[4] = {0, 0, 0, 0}; /* the root list (rs_chien_k), newest first; 0 past the last */
+        uint32_t rl[4] = {0, 0, 0, 0};
         if (fast) {
             o4 = reinterpret_cast<const uint4 *>(om)[cw];
             l4 = reinterpret_cast<const uint4 *>(lam)[cw];
@@ -504,100 +508,68 @@ __global__ __launch_bounds__(FWG, FORNEY_WAVES) void rs_forney_k(const RsDevTabl
             rl[0] = ra.x, rl[1] = ra.y, rl[2] = ra.z, rl[3] = ra.w;
         }
         const uint32_t ow[4] = {o4.x, o4.y, o4.z, o4.w}, lw[4] = {l4.x, l4.y, l4.z, l4.w};
-        /* address-form logs: Omega_m packed two per register, and the
-         * derivative terms Lambda_(2h+1) for 2h <= dtop = (deg - 1) & ~1 */
-        uint32_t omp[8], lod[4];
-#pragma unroll
-        for (int m = 0; m < 16; m += 2)
-            omp[m >> 1] = gf.afrom((ow[m >> 2] >> (8 * (m & 3))) & 0xffu) |
-                          (gf.afrom((ow[(m + 1) >> 2] >> (8 * ((m + 1) & 3))) & 0xffu) << 16);
         const uint32_t dtop = deg ? (deg - 1u) & ~1u : 0u;
+        uint32_t opu[16], lod[8]; /* address-form logs: Omega_m; Lambda_(2h+1) for 2h <= dtop */
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const int jl = 4 * q + 1, jh = 4 * q + 3; /* Lambda_j = byte j - 1 */
-            const uint32_t lo =
-                (uint32_t)(4 * q) <= dtop ? gf.afrom((lw[(jl - 1) >> 2] >> (8 * ((jl - 1) & 3))) & 0xffu) : gf.az();
-            const uint32_t hi =
-                (uint32_t)(4 * q + 2) <= dtop ? gf.afrom((lw[(jh - 1) >> 2] >> (8 * ((jh - 1) & 3))) & 0xffu)
-                                              : gf.az();
-            lod[q] = lo | (hi << 16);
-        }
-#define OMLOG(m) (((m) & 1) ? (omp[(m) >> 1] >> 16) : (omp[(m) >> 1] & 0xffffu))
-#define LODD(h) (((h) & 1) ? (lod[(h) >> 1] >> 16) : (lod[(h) >> 1] & 0xffffu))
+        for (int m = 0; m < 16; ++m)
+            opu[m] = gf.afrom((ow[m >> 2] >> (8 * (m & 3))) & 0xffu);
+#pragma unroll
+        for (int h = 0; h < 8; ++h)
+            lod[h] = (uint32_t)(2 * h) <= dtop ? gf.afrom((lw[(2 * h) >> 2] >> (8 * ((2 * h) & 3))) & 0xffu) : gf.az();
         const uint32_t degmax = wave_max(deg);
-        const uint32_t nir = max(degmax, wave_max(dtop) + 1u); /* powers i m needed: m < nir */
-        /* phase 1: every root's location byte and magnitude, packed four per
-         * register (the roots' loop is unrolled: FORNEY_R per step, steps past
-         * the wave's degree skipped) */
         uint32_t posp[4] = {0, 0, 0, 0}, magp[4] = {0, 0, 0, 0};
         uint32_t fixed = 0;
 #pragma unroll
-        for (int n = 0; n < 16; n += FORNEY_R) {
-            if ((uint32_t)n >= degmax) /* uniform */
+        for (int n0 = 0; n0 < 16; n0 += R) {
+            if ((uint32_t)n0 >= degmax) /* uniform */
                 continue;
-            uint32_t ir[FORNEY_R];
+            uint32_t ir[R], si[R], s[R], num[R], den[R], nh[R], dh[R];
 #pragma unroll
-            for (int t = 0; t < FORNEY_R; ++t) /* any order: roots are independent */
-                ir[t] = root_point((rl[(n + t) >> 2] >> (8 * ((n + t) & 3))) & 0xffu);
-            /* powers alpha^(i m) as plain scaled logs 128 (i m mod 255), even
-             * and odd m in two chains */
-            uint32_t i2[FORNEY_R], ie[FORNEY_R], io[FORNEY_R], nm[FORNEY_R], den[FORNEY_R];
-#pragma unroll
-            for (int t = 0; t < FORNEY_R; ++t) {
-                const uint32_t i1 = ir[t] == 255u ? 0u : ir[t];
-                i2[t] = red(i1 + i1) << 7;
-                ie[t] = 0;
-                io[t] = i1 << 7;
-                nm[t] = 0;
-                den[t] = 0;
+            for (int t = 0; t < R; ++t) {
+                ir[t] = root_point((rl[(n0 + t) >> 2] >> (8 * ((n0 + t) & 3))) & 0xffu);
+                si[t] = 128u * (ir[t] == 255u ? 0u : ir[t]);
+                s[t] = num[t] = den[t] = nh[t] = dh[t] = 0;
             }
 #pragma unroll
-            for (int m0 = 0; m0 < 16; m0 += 4) {
-                if ((uint32_t)m0 < nir) {
+            for (int b = 0; b < 8; ++b) {
 #pragma unroll
-                    for (int m = m0; m < m0 + 4; m += 2) {
-#pragma unroll
-                        for (int t = 0; t < FORNEY_R; ++t) {
-                            nm[t] ^= gf.expa(OMLOG(m) + ie[t]);
-                            den[t] ^= gf.expa(LODD(m >> 1) + ie[t]);
-                            nm[t] ^= gf.expa(OMLOG(m + 1) + io[t]);
-                            ie[t] = addmod7(ie[t], i2[t]);
-                            io[t] = addmod7(io[t], i2[t]);
-                        }
+                for (int t = 0; t < R; ++t) {
+                    num[t] ^= gf.expa(opu[b] + s[t]);
+                    nh[t] ^= gf.expa(opu[b + 8] + s[t]);
+                    if ((b & 1) == 0) {
+                        den[t] ^= gf.expa(lod[b >> 1] + s[t]);
+                        dh[t] ^= gf.expa(lod[(b >> 1) + 4] + s[t]);
                     }
+                    s[t] = addmod7(s[t], si[t]);
                 }
-                __builtin_amdgcn_sched_barrier(0); /* one group of powers at a time: registers */
+                if (b & 1) {
+#pragma unroll
+                    for (int t = 0; t < R; ++t)
+                        asm volatile("" : "+v"(num[t]), "+v"(den[t]), "+v"(nh[t]), "+v"(dh[t]));
+                    __builtin_amdgcn_sched_barrier(0); /* two powers at a time: registers */
+                }
             }
 #pragma unroll
-            for (int t = 0; t < FORNEY_R; ++t) {
-                /* fcr = 1 (the default config): alpha^(i (fcr - 1)) = 1, log 0 */
+            for (int t = 0; t < R; ++t) { /* s = 128 (8 i mod 255) */
+                num[t] ^= gf.expa(gf.loga(nh[t]) + s[t]);
+                den[t] ^= gf.expa(gf.loga(dh[t]) + s[t]);
                 const uint32_t ln2 =
                     fcr1 ? 0u : mod255((uint32_t)((int32_t)ir[t] * ((int32_t)P.fcr - 1) + (int32_t)RS_NN));
                 const uint32_t lden = gf.plog(gf.loga(den[t])); /* log 0 = 255 in the reference: no den = 0 guard */
-                /* (log num + ln2 + 255 - log den) mod 255 -- sum < 765, one
-                 * reduction leaves it < 510, inside the exp table's two periods */
-                const uint32_t lm = red(gf.plog(gf.loga(nm[t])) + ln2 + RS_NN - lden);
-                const bool z = (uint32_t)(n + t) < deg && nm[t] != 0u; /* zero numerator: no correction, not counted */
+                const uint32_t lm = red(gf.plog(gf.loga(num[t])) + ln2 + RS_NN - lden);
+                const bool z = (uint32_t)(n0 + t) < deg && num[t] != 0u;
                 fixed += z ? 1u : 0u;
-                /* location k = (i iprim - 1) mod 255 (i = 1..255); iprim = 1: i - 1 */
                 const uint32_t k = iprim1 ? ir[t] - 1u : (ir[t] * P.iprim + 254u) % 255u;
-                const uint32_t p = (uint32_t)((int32_t)k - pad); /* < size + 32 */
-                posp[(n + t) >> 2] |= p << (8 * ((n + t) & 3));
-                magp[(n + t) >> 2] |= (z ? gf.exp(lm) : 0u) << (8 * ((n + t) & 3));
+                const uint32_t p = (uint32_t)((int32_t)k - pad);
+                posp[(n0 + t) >> 2] |= (p & 0xffu) << (8 * ((n0 + t) & 3));
+                magp[(n0 + t) >> 2] |= (z ? gf.exp(lm) : 0u) << (8 * ((n0 + t) & 3));
             }
             __builtin_amdgcn_sched_barrier(0);
         }
-        __builtin_amdgcn_sched_barrier(0);
-        /* the corrections go to rs_apply_k as a record: 16 location bytes,
-         * 16 magnitudes (0: nothing to apply); over the root map just read */
         if (fast) {
             uint4 *rec = reinterpret_cast<uint4 *>(roots + cw * 32u);
             rec[0] = make_uint4(posp[0], posp[1], posp[2], posp[3]);
             rec[1] = make_uint4(magp[0], magp[1], magp[2], magp[3]);
-        }
-#undef OMLOG
-#undef LODD
-        if (fast) {
             ok[cw] = 1;
             if (corrected)
                 corrected[cw] = (uint8_t)fixed;
@@ -1031,12 +1003,14 @@ extern "C" hipError_t rsk_forney(const RsDevTables *tab, const RsCorrParams *prm
 {
     if (count == 0)
         return hipSuccess;
+    const size_t need = (count + F2WG - 1) / F2WG, cap = FAST_ROUNDS * 2u * (size_t)(num_cu > 0 ? num_cu : 256);
+    const dim3 grid((uint32_t)(need < cap ? need : cap));
     if (prm->fcr == 1u && prm->iprim == 1u)
-        RS_LAUNCH(rs_forney_k<true>, dim3(fast_grid(count, num_cu)), dim3(FWG), 0, stream, tab, *prm, data,
-                           dstride, parity, pstride, count, ws->lam, ws->om, ws->roots, ws->meta, ok, corrected);
+        RS_LAUNCH(rs_forney_k<true>, grid, dim3(F2WG), 0, stream, tab, *prm, data, dstride, parity, pstride, count,
+                  ws->lam, ws->om, ws->roots, ws->meta, ok, corrected);
     else
-        RS_LAUNCH(rs_forney_k<false>, dim3(fast_grid(count, num_cu)), dim3(FWG), 0, stream, tab, *prm, data,
-                           dstride, parity, pstride, count, ws->lam, ws->om, ws->roots, ws->meta, ok, corrected);
+        RS_LAUNCH(rs_forney_k<false>, grid, dim3(F2WG), 0, stream, tab, *prm, data, dstride, parity, pstride, count,
+                  ws->lam, ws->om, ws->roots, ws->meta, ok, corrected);
     return hipGetLastError();
 }
 
