@@ -623,10 +623,6 @@ __global__ __launch_bounds__(EWG, ERA_WAVES) void rs_era_k(const RsDevTables *__
     __syncthreads();
     const GfA gf{lds_addr(lgf) + 4u * (threadIdx.x & 31u) + 1u};
     const uint32_t pofs = gf.pofs;
-    const uint32_t AZ = gf.az();
-    constexpr uint32_t M255 = 255u * 128u;
-    /* x mod 255 on scaled logs / address forms: x < 2 * 255 * 128 + 128 */
-    auto red7 = [](uint32_t x) __attribute__((always_inline)) { return min(x, x - M255); };
     const uint32_t lim = P.size + RS_NR, pad = (uint32_t)P.pad;
 
     uint32_t it = 0;
@@ -686,31 +682,35 @@ __global__ __launch_bounds__(EWG, ERA_WAVES) void rs_era_k(const RsDevTables *__
 
         /* ---- erasure locator, src/decode.c:31-47, as the product of two
          * halves A = prod_(l<16), B = prod_(l>=16) (the same field elements;
-         * 1,038 lookups instead of 1,395).  Each half incrementally:
-         * H_j += X_l H_(j-1), j = l+1 down to 1, the new top term X_l H_l
-         * (nonzero) one add of logs ---- */
+         * fewer lookups than one 32-factor product).  Each half
+         * incrementally: H_j += X_l H_(j-1), j = l+1 down to 1 ---- */
         constexpr int NH = RS_NR / 2;
         auto half_locator = [&](uint32_t (&h)[NH + 1], auto l0c) __attribute__((always_inline)) {
             constexpr int L0 = decltype(l0c)::value;
-            h[0] = pofs;
+            /* coefficients as log-entry addresses (GfA::hz): a term is the log
+             * of the old H_(j-1) (ds_read_u16) and the exp of the product, two
+             * lookups; the logs once at the end */
+            const uint32_t HZ = gf.hz();
+            h[0] = HZ + 128u;
 #pragma unroll
             for (int j = 1; j <= NH; ++j)
-                h[j] = AZ;
+                h[j] = HZ;
             static_for<0, NH, 1>([&](auto lc) __attribute__((always_inline)) {
                 constexpr int l = decltype(lc)::value, lg = L0 + l;
                 const uint32_t p = (pk[lg >> 2] >> (8 * (lg & 3))) & 0xffu;
                 const uint32_t xs = 128u * (254u - (p + pad)); /* scaled log X_l */
                 static_for<0, l + 1, 1>([&](auto kc) __attribute__((always_inline)) {
                     constexpr int j = l + 1 - decltype(kc)::value;
-                    if constexpr (j == l + 1)
-                        h[j] = red7(h[j - 1] + xs);
-                    else
-                        h[j] = gf.loga(gf.expa(h[j]) ^ gf.expa(h[j - 1] + xs));
+                    h[j] ^= shl7(gf.expa((j == 1 ? pofs : gf.logh(h[j - 1])) + xs));
                     if constexpr ((j & 7) == 0)
                         __builtin_amdgcn_sched_barrier(0); /* eight terms at a time: registers */
                 });
                 __builtin_amdgcn_sched_barrier(0); /* one factor at a time: registers */
             });
+            h[0] = pofs;
+#pragma unroll
+            for (int j = 1; j <= NH; ++j)
+                h[j] = gf.logh(h[j]);
         };
         uint32_t ha[NH + 1], hb[NH + 1]; /* address-form logs of A_0..16, B_0..16 */
         half_locator(ha, std::integral_constant<int, 0>{});
