@@ -443,9 +443,8 @@ __global__ __launch_bounds__(XWG, 4) void rs_chien32_k(const RsDevTables *__rest
 #pragma unroll
                     for (int k = 0; k < NT; k += 2) {
                         const lds_u32x4_t r1 = lds128(A[k]), r2 = lds128(A[k + 1]);
-                        const uint32_t t1 = A[k] + inc[k], t2 = A[k + 1] + inc[k + 1];
-                        A[k] = min(t1, t1 - WRAP);
-                        A[k + 1] = min(t2, t2 - WRAP);
+                        A[k] = chien_step<WRAP>(A[k], inc[k]);
+                        A[k + 1] = chien_step<WRAP>(A[k + 1], inc[k + 1]);
                         acc[0] = xor3(acc[0], r1.x, r2.x);
                         acc[1] = xor3(acc[1], r1.y, r2.y);
                         acc[2] = xor3(acc[2], r1.z, r2.z);

@@ -82,6 +82,24 @@ __device__ __forceinline__ void prio_by_progress(uint32_t it)
     }
 }
 
+/* (a + inc) reduced below WRAP = 255 * row bytes (a < WRAP, or the all-zero
+ * rows' WRAP + j stepping by WRAP; inc <= WRAP): the Chien row addresses.
+ * Three VOP2 ops (add, subtract with the borrow into VCC, select on VCC)
+ * instead of two adds and a half-rate v_min_u32: rs_chien_k 0.068 -> 0.062 ms
+ * (profiles/r03_chien_vcc.log) */
+template <uint32_t WRAP>
+__device__ __forceinline__ uint32_t chien_step(uint32_t a, uint32_t inc)
+{
+    uint32_t t1, t2, r;
+    asm("v_add_u32_e32 %0, %3, %4\n\t"
+        "v_subrev_co_u32_e32 %1, vcc, %5, %0\n\t"
+        "v_cndmask_b32_e32 %2, %1, %0, vcc"
+        : "=&v"(t1), "=&v"(t2), "=v"(r)
+        : "v"(a), "v"(inc), "i"(WRAP)
+        : "vcc");
+    return r;
+}
+
 /* a ^ b ^ c in one VALU op (gfx950 v_bitop3_b32, truth table 0x96) */
 __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c)
 {
