@@ -185,23 +185,33 @@ __global__ __launch_bounds__(BWG, BM_WAVES) void rs_bm_k(const RsDevTables *__re
             const uint32_t up = min((uint32_t)(NL - 1), max(dl, db + 1u));
             const uint32_t ub2 = wave_max_full(up);
             ubp = ub2;
-#pragma unroll
-            for (int m = (NL - 1) / 4; m >= 0; --m) {
+            const uint64_t lmask = __ballot(lengthen);
+            static_for<0, (NL - 1) / 4 + 1, 1>([&](auto mc) __attribute__((always_inline)) {
+                constexpr int m = (NL - 1) / 4 - decltype(mc)::value; /* top down */
                 if ((uint32_t)(4 * m) <= ub2) {
 #pragma unroll
-                    for (int i = 4 * m + 3; i >= 4 * m; --i) {
-                        if (i >= NL + 1)
-                            continue;
-                        if (i > 0 && i < NL) {
-                            uint32_t e7;
-                            const uint32_t e = gf.expa(dq + B[i - 1]);
-                            asm("v_lshlrev_b16 %0, 7, %1" : "=v"(e7) : "v"(e));
-                            hl[i] ^= e7;
-                        }
-                        B[i] = lengthen ? (i < NL ? la[i] : AZ) : (i > 0 ? B[i - 1] : AZ);
+                    for (int i = 4 * m + 3; i >= 4 * m; --i)
+                        if (i > 0 && i < NL)
+                            hl[i] ^= shl7(gf.expa(dq + B[i - 1]));
+                    /* B_i <- lengthen ? log Lambda_i (old) : B_(i-1), top down,
+                     * as VOP2 selects on VCC (the compiler's e64 selects on an
+                     * SGPR mask issue at half rate; 2 %, profiles/r03_bm_vccsel.log) */
+                    if constexpr (4 * m + 3 < NL) {
+                        const uint32_t b0 = m > 0 ? B[m > 0 ? 4 * m - 1 : 0] : AZ;
+                        asm("s_mov_b64 vcc, %8\n\t"
+                            "v_cndmask_b32_e32 %3, %2, %7, vcc\n\t"
+                            "v_cndmask_b32_e32 %2, %1, %6, vcc\n\t"
+                            "v_cndmask_b32_e32 %1, %0, %5, vcc\n\t"
+                            "v_cndmask_b32_e32 %0, %9, %4, vcc"
+                            : "+v"(B[4 * m]), "+v"(B[4 * m + 1]), "+v"(B[4 * m + 2]), "+v"(B[4 * m + 3])
+                            : "v"(la[4 * m]), "v"(la[4 * m + 1]), "v"(la[4 * m + 2]), "v"(la[4 * m + 3]),
+                              "s"(lmask), "v"(b0)
+                            : "vcc");
+                    } else {
+                        B[4 * m] = lengthen ? la[4 * m] : B[4 * m - 1]; /* B_16; B_17 plays no part */
                     }
                 }
-            }
+            });
             db = lengthen ? dl : min(db + 1u, (uint32_t)(NL - 1));
             if (upd)
                 dl = up;
