@@ -499,6 +499,7 @@ __global__ __launch_bounds__(F2WG, 6) void rs_forney_k(const RsDevTables *__rest
     const int32_t pad = P.pad;
     constexpr bool fcr1 = P11, iprim1 = P11;
     constexpr int R = 4;
+    const uint32_t mp = 255u * 128u + gf.pofs; /* alpha^(log a - log b) = expa(loga a - loga b + mp) */
 
     for (size_t base = (size_t)blockIdx.x * F2WG; base < count; base += (size_t)gridDim.x * F2WG) {
         const size_t cw = base + threadIdx.x;
@@ -562,16 +563,24 @@ __global__ __launch_bounds__(F2WG, 6) void rs_forney_k(const RsDevTables *__rest
             for (int t = 0; t < R; ++t) { /* s = 128 (8 i mod 255) */
                 num[t] ^= gf.expa(gf.loga(nh[t]) + s[t]);
                 den[t] ^= gf.expa(gf.loga(dh[t]) + s[t]);
-                const uint32_t ln2 =
-                    fcr1 ? 0u : mod255((uint32_t)((int32_t)ir[t] * ((int32_t)P.fcr - 1) + (int32_t)RS_NN));
-                const uint32_t lden = gf.plog(gf.loga(den[t])); /* log 0 = 255 in the reference: no den = 0 guard */
-                const uint32_t lm = red(gf.plog(gf.loga(num[t])) + ln2 + RS_NN - lden);
+                uint32_t mag;
+                if constexpr (fcr1) {
+                    /* alpha^(log num + 255 - log den) straight from the address
+                     * forms: 128 (log num - log den + 255) + pofs is inside the
+                     * exp table's two periods (den != 0 at the distinct roots of
+                     * the fast path) */
+                    mag = gf.expa(gf.loga(num[t]) - gf.loga(den[t]) + mp);
+                } else {
+                    const uint32_t ln2 = mod255((uint32_t)((int32_t)ir[t] * ((int32_t)P.fcr - 1) + (int32_t)RS_NN));
+                    const uint32_t lden = gf.plog(gf.loga(den[t])); /* log 0 = 255 in the reference: no den = 0 guard */
+                    mag = gf.exp(red(gf.plog(gf.loga(num[t])) + ln2 + RS_NN - lden));
+                }
                 const bool z = (uint32_t)(n0 + t) < deg && num[t] != 0u;
                 fixed += z ? 1u : 0u;
                 const uint32_t k = iprim1 ? ir[t] - 1u : (ir[t] * P.iprim + 254u) % 255u;
                 const uint32_t p = (uint32_t)((int32_t)k - pad);
                 posp[(n0 + t) >> 2] |= (p & 0xffu) << (8 * ((n0 + t) & 3));
-                magp[(n0 + t) >> 2] |= (z ? gf.exp(lm) : 0u) << (8 * ((n0 + t) & 3));
+                magp[(n0 + t) >> 2] |= (z ? mag : 0u) << (8 * ((n0 + t) & 3));
             }
             __builtin_amdgcn_sched_barrier(0);
         }
