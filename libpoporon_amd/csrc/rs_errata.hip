@@ -612,11 +612,15 @@ __global__ __launch_bounds__(XWG, 4) void rs_forney32_k(const RsDevTables *__res
             for (int t = 0; t < XR; ++t) { /* s = 128 (H i mod 255) */
                 num[t] ^= gf.expa(gf.loga(nh[t]) + s[t]);
                 den[t] ^= gf.expa(gf.loga(dh[t]) + s[t]);
-                const uint32_t ln2 = mod255((uint32_t)((int32_t)ir[t] * ((int32_t)P.fcr - 1) + (int32_t)RS_NN));
-                const uint32_t lnum = gf.plog(gf.loga(num[t])), lden = gf.plog(gf.loga(den[t]));
+                /* alpha^(log num + ln2 + 255 - log den) from the address forms
+                 * (den != 0 at the deg distinct roots), reduced once */
+                const uint32_t l2s = P.fcr == 1u ? 0u
+                                                 : 128u * mod255((uint32_t)((int32_t)ir[t] * ((int32_t)P.fcr - 1) +
+                                                                            (int32_t)RS_NN));
+                const uint32_t x = gf.loga(num[t]) - gf.loga(den[t]) + 255u * 128u + gf.pofs + l2s;
                 const bool z = (uint32_t)(n0 + t) < deg && num[t] != 0u;
                 fixed += z ? 1u : 0u;
-                magp[(n0 + t) >> 2] |= (z ? gf.exp((lnum + ln2 + RS_NN - lden) % 255u) : 0u) << (8 * ((n0 + t) & 3));
+                magp[(n0 + t) >> 2] |= (z ? gf.expa(min(x, x - 255u * 128u)) : 0u) << (8 * ((n0 + t) & 3));
             }
             __builtin_amdgcn_sched_barrier(0);
         }

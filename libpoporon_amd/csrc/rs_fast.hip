@@ -641,6 +641,7 @@ __global__ __launch_bounds__(EWG, ERA_WAVES) void rs_era_k(const RsDevTables *__
     __syncthreads();
     const GfA gf{lds_addr(lgf) + 4u * (threadIdx.x & 31u) + 1u};
     const uint32_t pofs = gf.pofs;
+    const uint32_t mp = 255u * 128u + pofs; /* alpha^(log a - log b) = expa(loga a - loga b + mp) */
     const uint32_t lim = P.size + RS_NR, pad = (uint32_t)P.pad;
 
     uint32_t it = 0;
@@ -865,11 +866,15 @@ __global__ __launch_bounds__(EWG, ERA_WAVES) void rs_era_k(const RsDevTables *__
             uint32_t cur[ERA_R / 4] = {};
 #pragma unroll
             for (int t = 0; t < ERA_R; ++t) {
-                const uint32_t ln2 = mod255((uint32_t)((int32_t)ii[t] * ((int32_t)P.fcr - 1) + (int32_t)RS_NN));
-                const uint32_t lnum = gf.plog(gf.loga(num[t])), lden = gf.plog(gf.loga(den[t]));
+                /* alpha^(log num + ln2 + 255 - log den) from the address forms
+                 * (den != 0 at the distinct erasure locations), reduced once */
+                const uint32_t l2s = P.fcr == 1u ? 0u
+                                                 : 128u * mod255((uint32_t)((int32_t)ii[t] * ((int32_t)P.fcr - 1) +
+                                                                            (int32_t)RS_NN));
+                const uint32_t x = gf.loga(num[t]) - gf.loga(den[t]) + mp + l2s;
                 const bool z = num[t] != 0u;
                 ncor += z ? 1u : 0u;
-                cur[t >> 2] |= (z ? gf.exp((lnum + ln2 + RS_NN - lden) % 255u) : 0u) << (8 * (t & 3));
+                cur[t >> 2] |= (z ? gf.expa(min(x, x - 255u * 128u)) : 0u) << (8 * (t & 3));
             }
             /* magnitude words through a shift register: the record's 32
              * bytes go out as two 16-byte stores (eight dword stores per
