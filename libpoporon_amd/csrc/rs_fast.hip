@@ -614,10 +614,11 @@ __global__ __launch_bounds__(F2WG, 6) void rs_forney_k(const RsDevTables *__rest
  * list (rs_correct_k in record mode).  Output: the 64-byte record of
  * rs_apply_k<32> (slots, magnitudes).
  *
- * Registers: the locator in 31 address-form logs, then packed two per
- * register for Omega (16 + 16 syndrome logs + 16 Omega); Forney reads Omega
- * and the odd Lambda terms unpacked (48 registers, 4 waves/SIMD: the kernel
- * is issue-bound, occupancy 4, 6 and 8 measured the same) and splits each
+ * Registers: the locator halves, then Lambda's and the syndromes' logs one
+ * register each for Omega (64 registers: plain adds instead of half-rate SDWA
+ * word selects, 2 %, profiles/r03_era_unpacked_ab.log); Forney reads Omega
+ * and the odd Lambda terms unpacked (48 registers, 4 waves/SIMD, 128 VGPRs:
+ * the kernel is issue-bound, occupancy 4, 6 and 8 measured the same) and splits each
  * sum at m = 16, so one 16-step power chain per root serves both halves
  * (0.36 -> 0.31-0.33 ms, profiles/r03_era_experiments.log); slots are
  * re-read where needed.
@@ -738,7 +739,7 @@ __global__ __launch_bounds__(EWG, ERA_WAVES) void rs_era_k(const RsDevTables *__
         for (int j = 0; j <= NH; ++j)
             hb[j] -= pofs; /* plain scaled logs (zero: SZ) */
         /* Lambda_k = sum_(i+j=k) A_i B_j, k < 32 (Lambda_32 plays no part) */
-        uint32_t alp[RS_NR / 2]; /* address-form logs of Lambda_0..31, two per register */
+        uint32_t alu[RS_NR]; /* address-form logs of Lambda_0..31 (one register each: plain adds below) */
         static_for<0, RS_NR, 1>([&](auto kc) __attribute__((always_inline)) {
             constexpr int k = decltype(kc)::value;
             uint32_t o = pofs;
@@ -750,15 +751,12 @@ __global__ __launch_bounds__(EWG, ERA_WAVES) void rs_era_k(const RsDevTables *__
                 asm volatile("" : "+v"(acc));
                 o = gf.loga(acc);
             }
-            if constexpr (k & 1)
-                alp[k >> 1] |= o << 16;
-            else
-                alp[k >> 1] = o;
+            alu[k] = o;
             __builtin_amdgcn_sched_barrier(0); /* one coefficient at a time: registers */
         });
 
         /* ---- Omega = S Lambda mod x^32, src/decode.c:147-158 ---- */
-        uint32_t sl[RS_NR / 2]; /* plain scaled logs of S_0..31, two per register */
+        uint32_t slu[RS_NR]; /* plain scaled logs of S_0..31 */
         {
             /* the syndromes again (L2): keeping them through the locator costs registers */
             const uint8_t *sp = syn + (valid ? cw : 0) * RS_NR;
@@ -767,23 +765,18 @@ __global__ __launch_bounds__(EWG, ERA_WAVES) void rs_era_k(const RsDevTables *__
             sb = reinterpret_cast<const uint4 *>(sp)[1];
             const uint32_t sw[8] = {sa.x, sa.y, sa.z, sa.w, sb.x, sb.y, sb.z, sb.w};
 #pragma unroll
-            for (int k = 0; k < RS_NR; k += 2)
-                sl[k >> 1] = gf.logs((sw[k >> 2] >> (8 * (k & 3))) & 0xffu) |
-                             (gf.logs((sw[k >> 2] >> (8 * ((k + 1) & 3))) & 0xffu) << 16);
+            for (int k = 0; k < RS_NR; ++k)
+                slu[k] = gf.logs((sw[k >> 2] >> (8 * (k & 3))) & 0xffu);
         }
         uint32_t ob[RS_NR / 4]; /* byte logs of Omega_0..31 (255 = zero), four per register */
         static_for<0, RS_NR, 1>([&](auto mc) __attribute__((always_inline)) {
             constexpr int m = decltype(mc)::value;
-            /* opaque per coefficient: halves unpacked at their use, not all at once */
-#pragma unroll
-            for (int k = 0; k < RS_NR / 2; ++k)
-                asm volatile("" : "+v"(alp[k]), "+v"(sl[k]));
             uint32_t acc = 0;
             static_for<0, m + 1, ERA_OG>([&](auto gc) __attribute__((always_inline)) {
                 constexpr int g = decltype(gc)::value; /* eight lookups at a time: registers */
 #pragma unroll
                 for (int t = g; t <= m && t < g + ERA_OG; ++t)
-                    acc ^= gf.expa(half(alp, t) + half(sl, m - t));
+                    acc ^= gf.expa(alu[t] + slu[m - t]);
                 asm volatile("" : "+v"(acc)); /* the sum now: no deferred xor tree */
                 __builtin_amdgcn_sched_barrier(0);
             });
@@ -794,15 +787,6 @@ __global__ __launch_bounds__(EWG, ERA_WAVES) void rs_era_k(const RsDevTables *__
                 ob[m >> 2] |= o << (8 * (m & 3));
             __builtin_amdgcn_sched_barrier(0); /* one coefficient's lookups at a time: registers */
         });
-        uint32_t op[RS_NR / 2]; /* Omega_0..31 address-form, two per register */
-#pragma unroll
-        for (int k = 0; k < RS_NR / 2; ++k)
-            op[k] = gf.afrom((ob[k >> 1] >> (16 * (k & 1))) & 0xffu) |
-                    (gf.afrom((ob[k >> 1] >> (16 * (k & 1) + 8)) & 0xffu) << 16);
-        uint32_t alo[RS_NR / 4]; /* Lambda_1, 3, .., 31 */
-#pragma unroll
-        for (int k = 0; k < RS_NR / 4; ++k)
-            alo[k] = (alp[2 * k] >> 16) | (alp[2 * k + 1] & 0xffff0000u);
 
         /* ---- Forney at the known roots, src/decode.c:159-191: num = sum_m
          * Omega_m alpha^(i m), den = sum_h Lambda_(2h+1) alpha^(2h i),
@@ -810,13 +794,13 @@ __global__ __launch_bounds__(EWG, ERA_WAVES) void rs_era_k(const RsDevTables *__
          * a zero numerator corrects nothing and is not counted ---- */
         uint32_t ncor = 0, mrec[RS_NR / 4];
         const uint32_t *slw = reinterpret_cast<const uint32_t *>(slots);
-        uint32_t opu[RS_NR], alou[RS_NR / 2]; /* unpacked once: plain adds in the loop, not SDWA word selects */
+        uint32_t opu[RS_NR], alou[RS_NR / 2]; /* unpacked: plain adds in the loop, not SDWA word selects */
 #pragma unroll
         for (int m = 0; m < RS_NR; ++m)
-            opu[m] = half(op, m);
+            opu[m] = gf.afrom((ob[m >> 2] >> (8 * (m & 3))) & 0xffu);
 #pragma unroll
         for (int h = 0; h < RS_NR / 2; ++h)
-            alou[h] = half(alo, h);
+            alou[h] = alu[2 * h + 1];
 #pragma unroll 1
         for (uint32_t q = 0; q < RS_NR / ERA_R; ++q) {
             uint32_t w[ERA_R / 4];
