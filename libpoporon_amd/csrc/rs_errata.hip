@@ -290,14 +290,13 @@ __global__ __launch_bounds__(XWG, 4) void rs_ebm_k(const RsDevTables *__restrict
             ob[k] = 0xFFFFFFFFu;
         const uint32_t degmax = wave_max_full(fast ? deg : 0u);
         if (degmax) {
-            uint32_t sl[RS_NR / 2]; /* plain scaled logs of S_0..S_31, two per register */
+            uint32_t sl[RS_NR]; /* plain scaled logs of S_0..S_31, one register each */
             {
                 const uint4 s4a = reinterpret_cast<const uint4 *>(sp)[0], s4b = reinterpret_cast<const uint4 *>(sp)[1];
                 const uint32_t sw[8] = {s4a.x, s4a.y, s4a.z, s4a.w, s4b.x, s4b.y, s4b.z, s4b.w};
 #pragma unroll
-                for (int k = 0; k < RS_NR; k += 2)
-                    sl[k >> 1] = gf.logs((sw[k >> 2] >> (8 * (k & 3))) & 0xffu) |
-                                 (gf.logs((sw[k >> 2] >> (8 * ((k + 1) & 3))) & 0xffu) << 16);
+                for (int k = 0; k < RS_NR; ++k)
+                    sl[k] = gf.logs((sw[k >> 2] >> (8 * (k & 3))) & 0xffu);
             }
 #pragma unroll
             for (int m = 0; m < RS_NR; ++m) {
@@ -305,7 +304,7 @@ __global__ __launch_bounds__(XWG, 4) void rs_ebm_k(const RsDevTables *__restrict
                     uint32_t acc = 0;
 #pragma unroll
                     for (int j = 0; j <= m; ++j)
-                        acc ^= gf.expa(al[j] + half(sl, m - j));
+                        acc ^= gf.expa(al[j] + sl[m - j]);
                     const uint32_t o = (uint32_t)m < deg ? gf.plog(gf.loga(acc)) : 255u;
                     ob[m >> 2] ^= (o ^ 0xffu) << (8 * (m & 3));
                 }

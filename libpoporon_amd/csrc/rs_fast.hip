@@ -259,18 +259,17 @@ __global__ __launch_bounds__(BWG, BM_WAVES) void rs_bm_k(const RsDevTables *__re
             const uint32_t sw[4] = {s4.x, s4.y, s4.z, s4.w};
             auto omega = [&](auto dmc) __attribute__((always_inline)) {
                 constexpr int DM = decltype(dmc)::value; /* > 0: every lane's bound is DM (no guards) */
-                uint32_t sl[8]; /* plain scaled logs of S_0..S_15, two per register */
+                uint32_t sl[16]; /* plain scaled logs of S_0..S_15, one register each */
 #pragma unroll
-                for (int k = 0; k < 16; k += 2)
-                    sl[k >> 1] = gf.logs((sw[k >> 2] >> (8 * (k & 3))) & 0xffu) |
-                                 (gf.logs((sw[k >> 2] >> (8 * ((k + 1) & 3))) & 0xffu) << 16);
+                for (int k = 0; k < 16; ++k)
+                    sl[k] = gf.logs((sw[k >> 2] >> (8 * (k & 3))) & 0xffu);
 #pragma unroll
                 for (int m = 0; m < 16; ++m) {
                     if (DM ? m < DM : (uint32_t)m < degmax) {
                         uint32_t acc = 0;
 #pragma unroll
                         for (int j = 0; j <= m; ++j)
-                            acc ^= gf.expa(al[j] + half(sl, m - j));
+                            acc ^= gf.expa(al[j] + sl[m - j]);
                         const uint32_t o = (uint32_t)m < deg ? gf.plog(gf.loga(acc)) : 255u;
                         ob[m >> 2] ^= (o ^ 0xffu) << (8 * (m & 3));
                     }
