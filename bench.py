@@ -58,7 +58,8 @@ METRIC = "RS(255,223) codewords/s (encode; decode @ t=16 errs) and GB/s vs HBM p
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
 CW_BYTES = 255         # algorithmic bytes per codeword
 K, NR, N = 223, 32, 255
-SEED = 0x5EED0001      # messages; errors: SEED + 1; erasures: SEED + 2; configs[4]: SEED + 4 / + 5
+SEED = 0x5EED0001      # messages; errors: SEED + 1; erasures: SEED + 2; configs[4]: SEED + 4 / + 5; mixed: + 9 / + 10
+MIXED_P, MIXED_CAP = 0.045, 24  # the mixed channel: binomial(255, p) errors per codeword, capped
 M64 = (1 << 64) - 1
 
 
@@ -76,6 +77,7 @@ def parse_args(argv=None):
     ap.add_argument("--no-c4", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-erasure", action="store_true")
+    ap.add_argument("--no-mixed", action="store_true", help="skip the mixed-channel decode (binomial error counts)")
     ap.add_argument("--no-host", action="store_true", help="skip the host-memory (PCIe) pipeline rates")
     ap.add_argument("--no-latency", action="store_true", help="skip the single-codeword call latency")
     ap.add_argument("--backend", default="", help="tests only: module with a CPU Backend (see docstring)")
@@ -98,6 +100,7 @@ PATHS = {
     "decode16": (K_REMAINDER, K_BM, K_CHIEN, K_FORNEY, K_APPLY, K_LIST, K_CORRECT),
     "erasure32": (K_REMAINDER, K_ERASURE, K_BM, K_CHIEN, K_FORNEY, K_LIST, K_APPLY, K_CORRECT),
     "errata16e8": (K_REMAINDER, K_ERASURE, K_BM, K_CHIEN, K_FORNEY, K_LIST, K_APPLY, K_CORRECT),
+    "decode_mixed": (K_REMAINDER, K_BM, K_CHIEN, K_FORNEY, K_APPLY, K_LIST, K_CORRECT),
 }
 
 
@@ -312,6 +315,27 @@ class GpuBackend:
     def n_diff(self, a, b):
         return int((a != b).any(dim=1).sum())
 
+    def host(self, t, idx):
+        """rows idx of a device tensor, as numpy"""
+        return t[self.torch.as_tensor(idx, device=self.dev)].cpu().numpy()
+
+    def from_host(self, a):
+        return self.torch.from_numpy(a).to(self.dev)
+
+    def mask_errors(self, mag, ne):
+        """zero the magnitudes past each row's error count (the channel then skips them)"""
+        k = self.torch.arange(mag.shape[1], device=self.dev)
+        mag.mul_((k[None, :] < ne[:, None].long()).to(self.torch.uint8))
+
+    def n_bad_mixed(self, st, ne, out, clean):
+        """codewords with <= 16 errors not restored with ok = 1 and corrected = their count"""
+        ok, cor = st
+        bad = (ne <= 16) & ((ok != 1) | (cor != ne) | (out != clean).any(dim=1))
+        return int(bad.sum())
+
+    def count_ok(self, st):
+        return int(st[0].sum())
+
     def free_bytes(self):
         return self.torch.cuda.mem_get_info(self.dev)[0]
 
@@ -441,12 +465,20 @@ def run_weak(be, ranks, args, rank, world):
         kt = {k: be.rs.timing_read(k) for k in be.P.KERNEL_NAMES}
         be.rs.timing(False)
     nbad = be.n_bad(st, 16) + sum(be.n_diff(b, clean) for b in enc)
-    nbad += sum(be.n_diff(b, clean) for b in (bad[args.warmup:args.warmup + (2 if elapsed_ev else 1) * args.steps]
-                                              if copies else [cw]))
+    timed = bad[args.warmup:args.warmup + (2 if elapsed_ev else 1) * args.steps] if copies else [cw]
+    nbad += sum(be.n_diff(b, clean) for b in timed)
+    # parity sample: every SAMPLE_STRIDE-th codeword's timed
+    # encode and decode, checked against the reference after the timed loops
+    idx = sample_index(B)
+    rows = be.host(clean, idx)
+    samples = {"encode": {"msg": rows[:, :K], "got_par": rows[:, K:], "first": first},
+               "decode16": {"in": channel_rows(rows, be.host(err[0], idx), be.host(err[1], idx)),
+                            "out": be.host(timed[-1], idx), "ok": be.host(st[0], idx), "cor": be.host(st[1], idx),
+                            "first": first}}
     csum = be.checksum(cw, first)
     del bad, enc
     return {"elapsed": elapsed, "elapsed_ev": elapsed_ev, "kt": kt, "nbad": ranks.sum_int(nbad), "copies": copies,
-            "checksum": ranks.sum_u64(csum), "cw": cw, "clean": clean, "err": err, "st": st}
+            "checksum": ranks.sum_u64(csum), "cw": cw, "clean": clean, "err": err, "st": st, "samples": samples}
 
 
 def run_erasure(be, ranks, args, rank, world, w, ne=32, nerr=0):
@@ -507,6 +539,11 @@ def run_erasure(be, ranks, args, rank, world, w, ne=32, nerr=0):
     if not nerr:
         enbad += sum(be.n_diff(b, eclean) for b in (ebad[1:] if ecopies else [cw]))
     enbad = ranks.sum_int(enbad)
+    idx = sample_index(B)
+    sample = {"in": channel_rows(be.host(eclean, idx), be.host(pos, idx), be.host(emag, idx)),
+              "out": be.host(ebad[es] if ecopies else cw, idx), "ok": be.host(w["st"][0], idx),
+              "cor": be.host(w["st"][1], idx), "slots": be.host(slots, idx), "cnt": be.host(cnts, idx),
+              "first": first}
     return {"cw_per_s": round(B * world * es / et, 1),
             "kernel_cw_per_s_per_gpu": round(B / (kms * 1e-3), 1) if kms else None,
             "kernels_avg_ms": {be.P.KERNEL_NAMES[k]: round(ms / n, 4) for k, (ms, n) in ekt.items()},
@@ -515,7 +552,190 @@ def run_erasure(be, ranks, args, rank, world, w, ne=32, nerr=0):
             "verified": enbad == 0,
             "channel": "outside the timed decodes (one corrupted copy per decode)" if ecopies
             else "in place, inside the timed decodes",
-            "_kt": ekt, "_steps": es}
+            "_kt": ekt, "_steps": es, "_sample": sample}
+
+
+def mixed_counts(first, n):
+    """Errors per codeword of the mixed channel: the binomial(255, MIXED_P)
+    quantile of a counter hash of the global codeword index (so any sharding
+    reproduces it), capped at MIXED_CAP."""
+    import numpy as np
+    from scipy.stats import binom
+
+    import testutil as T
+    h = T.synth_rows_cpu(SEED + 9, first, n, 4).astype(np.uint32)
+    u = (h[:, 0] | (h[:, 1] << 8) | (h[:, 2] << 16) | (h[:, 3] << 24)).astype(np.float64)
+    ne = binom.ppf((u + 0.5) / 4294967296.0, N, MIXED_P)
+    return np.minimum(ne, MIXED_CAP).astype(np.uint8)
+
+
+def run_mixed(be, ranks, args, rank, world, w):
+    """A realistic channel: binomial(255, MIXED_P) errors per codeword, capped
+    at MIXED_CAP (mean ~11.5; ~6-7 % of the codewords past t = 16, which the
+    split kernels hand to the general kernel's list -- failures and the
+    reference's miscorrections).  Codewords with <= 16 errors must come back
+    restored with ok = 1 and corrected = their error count; every codeword's
+    bytes, ok and count are in the parity sample against the reference."""
+    B = args.batch
+    first = rank * B
+    ne_h = mixed_counts(first, B)
+    pos, mag = be.errors(first, B, MIXED_CAP, N, SEED + 10)
+    ne = be.from_host(ne_h)
+    be.mask_errors(mag, ne)
+    cw = w["clean"]
+    es = max(3, args.steps // 2)
+    mcopies = (es + 1) * B * N <= 0.5 * be.free_bytes()
+    mbad = []
+    for _ in range(es + 1 if mcopies else 1):
+        b = be.like(cw)
+        be.copy(b, cw)
+        be.channel(b, (pos, mag))
+        mbad.append(b)
+    st = be.status(B)
+
+    def mstep(k):
+        if mcopies:
+            d = mbad[k]
+        else:
+            be.copy(mbad[0], cw)
+            be.channel(mbad[0], (pos, mag))
+            d = mbad[0]
+        be.decode(d, st)
+
+    mstep(0)
+    ranks.barrier(be.sync)
+    gpu = be.kind == "gpu"
+    if gpu:
+        be.rs.timing(True)
+    t0 = time.perf_counter()
+    for k in range(es):
+        mstep(1 + k if mcopies else 0)
+    ranks.barrier(be.sync)
+    et = ranks.max(time.perf_counter() - t0)
+    mkt = {}
+    if gpu:
+        mkt = {k: be.rs.timing_read(k) for k in be.P.KERNEL_NAMES}
+        mkt = {k: v for k, v in mkt.items() if v[1]}
+        be.rs.timing(False)
+    last = mbad[es] if mcopies else mbad[0]
+    nbad = ranks.sum_int(be.n_bad_mixed(st, ne, last, cw))
+    idx = sample_index(B)
+    sample = {"in": channel_rows(be.host(cw, idx), be.host(pos, idx), be.host(mag, idx)), "out": be.host(last, idx),
+              "ok": be.host(st[0], idx), "cor": be.host(st[1], idx), "first": first}
+    past = ranks.sum_int(int((ne_h > 16).sum()))
+    okn = ranks.sum_int(be.count_ok(st))
+    kms = sum(ms / es for ms, n in mkt.values())
+    lst = mkt.get(be.P.KERNEL_LIST, (0.0, 0))[0] / es if gpu else 0.0
+    return {"cw_per_s": round(B * world * es / et, 1),
+            "kernel_cw_per_s_per_gpu": round(B / (kms * 1e-3), 1) if kms else None,
+            "kernels_avg_ms": {be.P.KERNEL_NAMES[k]: round(ms / n, 4) for k, (ms, n) in mkt.items()} if gpu else {},
+            "list_kernel_share": round(lst / kms, 4) if kms else None,
+            "channel": f"binomial({N}, {MIXED_P}) errors per codeword (capped at {MIXED_CAP}), unique positions, "
+                       "magnitudes in [1,255]",
+            "mean_errors": round(float(ne_h.mean()), 3),
+            "past_t_fraction": round(past / (B * world), 4),
+            "ok_fraction": round(okn / (B * world), 4),
+            "verified": nbad == 0,
+            "_kt": mkt, "_steps": es, "_sample": sample}
+
+
+# ----------------------------------------------------------------------------
+# parity sample against the reference CPU path (SURVEY 8(d) "GPU timing")
+# ----------------------------------------------------------------------------
+SAMPLE_STRIDE = 4096
+
+
+def sample_index(B):
+    import numpy as np
+    return np.arange(0, B, SAMPLE_STRIDE, dtype=np.int64)
+
+
+def channel_rows(rows, pos, mag):
+    import numpy as np
+    out = rows.copy()
+    out[np.arange(rows.shape[0])[:, None], pos.astype(np.int64)] ^= mag
+    return out
+
+
+class ParityChecker:
+    """The checker of the bench's parity sample: the reference itself
+    (oracle/_ref/libpoporon_ref.so, libpoporon compiled from /root/reference/src,
+    driven through its public single-codeword API: poporon_encode /
+    poporon_decode, erasure lists via poporon_erasure_*) where it was built,
+    else the clean-room restatement pinned to the reference's golden vectors
+    (oracle/rs_oracle.c).  Runs after every timed loop; never on the codec path."""
+
+    def __init__(self):
+        from oracle import Oracle, Reference, reference_available
+        self.kind = "reference" if reference_available() else "port"
+        if self.kind == "reference":
+            self.ref = Reference()
+            self.eref = Reference(erasure=True)
+        else:
+            self.o = Oracle()
+
+    def encode(self, msgs):
+        import numpy as np
+        if self.kind == "port":
+            return self.o.encode_batch(msgs)
+        return np.stack([self.ref.encode(m)[1] for m in msgs]) if len(msgs) else np.zeros((0, NR), np.uint8)
+
+    def decode(self, rows, slots=None, cnt=None):
+        """-> ok u8[n], corrected u8[n], rows' (data || parity) as the reference leaves them"""
+        import numpy as np
+        n = rows.shape[0]
+        if self.kind == "port":
+            if slots is None:
+                ok, cor, d, p = self.o.decode_batch(rows[:, :K], rows[:, K:])
+            else:
+                ok, cor, d, p = self.o.decode_batch(rows[:, :K], rows[:, K:], slots.astype(np.uint32),
+                                                    cnt.astype(np.uint32))
+            return ok, cor.astype(np.uint8), np.concatenate([d, p], 1)
+        ok, cor, out = np.zeros(n, np.uint8), np.zeros(n, np.uint8), rows.copy()
+        for c in range(n):
+            h = self.ref
+            if slots is not None and int(slots[c].max()) >= K:
+                # a slot past the message: the reference writes past the
+                # caller's buffer there (quirk Q4, undefined) -- the pinned
+                # restatement (which defines it) checks this row
+                from oracle import Oracle
+                r = Oracle().decode_batch(rows[c:c + 1, :K], rows[c:c + 1, K:], slots[c:c + 1].astype(np.uint32),
+                                          cnt[c:c + 1].astype(np.uint32))
+                r = (r[0][0], r[1][0], r[2][0], r[3][0])
+                ok[c], cor[c] = r[0], r[1]
+                out[c, :K], out[c, K:] = r[2], r[3]
+                continue
+            if slots is not None:
+                h = self.eref
+                # the batch API's slots past the count are the list's stale
+                # entries of the reference (quirks Q1/Q2): fill all, then reset
+                h.set_erasures(slots[c])
+                h.set_erasures(slots[c][: int(cnt[c])])
+            r = h.decode(rows[c, :K], rows[c, K:])
+            ok[c], cor[c] = r[0], r[1]
+            out[c, :K], out[c, K:] = r[2], r[3]
+        return ok, cor, out
+
+    def check(self, sm):
+        """number of sampled codewords whose GPU result differs from the checker's"""
+        import numpy as np
+        if "msg" in sm:
+            return int((self.encode(sm["msg"]) != sm["got_par"]).any(1).sum())
+        ok, cor, out = self.decode(sm["in"], sm.get("slots"), sm.get("cnt"))
+        bad = (ok != sm["ok"]) | (cor != sm["cor"]) | (out != sm["out"]).any(1)
+        return int(bad.sum())
+
+
+def parity_sample(samples, ranks):
+    chk = ParityChecker()
+    res = {"checker": ("reference: libpoporon compiled from /root/reference/src (oracle/_ref), public API"
+                       if chk.kind == "reference" else
+                       "port: clean-room restatement oracle/rs_oracle.c, pinned to the reference's golden vectors"),
+           "stride": SAMPLE_STRIDE, "compares": "parity bytes (encode); decoded bytes, ok and corrected_num (decode)"}
+    for mode, sm in samples.items():
+        n = len(sm["msg"] if "msg" in sm else sm["in"])
+        res[mode] = {"n": ranks.sum_int(n), "mismatches": ranks.sum_int(chk.check(sm))}
+    return res
 
 
 # ----------------------------------------------------------------------------
@@ -742,8 +962,11 @@ def main(argv=None):
                                f"{args.c4_total}-codeword strong split) under 'configs4'",
                    "codewords_per_gpu": B, "layout": "255-byte codeword rows, stride 255",
                    "code": "poporon_config_rs_default (8, 0x11D, fcr 1, prim 1, 32 roots)"},
-        "GB_per_s": round(value * CW_BYTES / 1e9, 2),
-        "hbm_frac_of_peak": round(value * CW_BYTES / 1e9 / (HBM_PEAK_GBS * world), 4),
+        # one bandwidth definition everywhere: 255 B per codeword
+        # per mode, so a round trip (encode + decode) counts 510 B
+        "GB_per_s": round(value * 2 * CW_BYTES / 1e9, 2),
+        "hbm_frac_of_peak": round(value * 2 * CW_BYTES / 1e9 / (HBM_PEAK_GBS * world), 4),
+        "bytes_per_unit": "510 = 255 (encode: 223 read + 32 written) + 255 (decode: 255 read) per round trip",
         "step": f"encode {B} messages + decode {B} corrupted codewords (16 errors each); the test channel corrupts "
                 "one copy per step before the timed loops; `value` / `ms_per_step` from a loop without per-kernel "
                 "events, per-kernel times and the roofline from a second loop of the same steps with HIP events "
@@ -752,6 +975,12 @@ def main(argv=None):
         "verified": w["nbad"] == 0,
         "weak_checksum": w["checksum"],
     }
+    samples = dict(w.pop("samples"))
+    if not args.no_mixed:
+        mix = run_mixed(be, ranks, args, rank, world, w)
+        samples["decode_mixed"] = mix.pop("_sample")
+        line["decode_mixed"] = mix
+        line["verified"] = line["verified"] and mix["verified"]
     if gpu and w["kt"]:
         P = be.P
         kt = {k: v for k, v in w["kt"].items() if v[1]}
@@ -775,26 +1004,35 @@ def main(argv=None):
         if not args.no_erasure:
             era = run_erasure(be, ranks, args, rank, world, w)
             modes["erasure32"] = path_roofline("erasure32", era.pop("_kt"), era.pop("_steps"), B, traffic)
+            samples["erasure32"] = era.pop("_sample")
             line["erasure_decode_32"] = era
             eta = run_erasure(be, ranks, args, rank, world, w, ne=16, nerr=8)
             modes["errata16e8"] = path_roofline("errata16e8", eta.pop("_kt"), eta.pop("_steps"), B, traffic)
+            samples["errata16e8"] = eta.pop("_sample")
             line["errata_decode_16e8"] = eta
-            line["verified"] = line["verified"] and era["verified"]
-        rt_ms = modes["encode"]["path_ms"] + modes["decode16"]["path_ms"]
-        rt = 2 * B * CW_BYTES / (rt_ms * 1e-3) / 1e9
-        modes["roundtrip"] = {"achieved": round(rt, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                              "frac": round(rt / HBM_PEAK_GBS, 4), "path_ms": round(rt_ms, 4),
-                              "algorithmic_bytes": 2 * B * CW_BYTES,
-                              "traffic": (modes["encode"]["traffic"] + modes["decode16"]["traffic"]
-                                          if modes["encode"]["traffic"] and modes["decode16"]["traffic"] else None),
-                              "note": "encode path + decode16 path, 255 B per codeword per mode"}
-        roof = dict(modes["decode16"])
-        roof.update({"kernel": "decode16 path (" + " + ".join(P.KERNEL_NAMES[k] for k in roof["kernels_ms"]) + ")",
+            line["verified"] = line["verified"] and era["verified"] and eta["verified"]
+        if "decode_mixed" in line:
+            modes["decode_mixed"] = path_roofline("decode_mixed", line["decode_mixed"].pop("_kt"),
+                                                  line["decode_mixed"].pop("_steps"), B, traffic)
+        if modes["encode"] and modes["decode16"]:
+            rt_ms = modes["encode"]["path_ms"] + modes["decode16"]["path_ms"]
+            rt = 2 * B * CW_BYTES / (rt_ms * 1e-3) / 1e9
+            modes["roundtrip"] = {"achieved": round(rt, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                  "frac": round(rt / HBM_PEAK_GBS, 4), "path_ms": round(rt_ms, 4),
+                                  "algorithmic_bytes": 2 * B * CW_BYTES,
+                                  "traffic": (modes["encode"]["traffic"] + modes["decode16"]["traffic"]
+                                              if modes["encode"]["traffic"] and modes["decode16"]["traffic"]
+                                              else None),
+                                  "note": "encode path + decode16 path, 255 B per codeword per mode"}
+        modes = {k: v for k, v in modes.items() if v}
+        roof = dict(modes.get("decode16") or {})
+        roof.update({"kernel": "decode16 path (" + " + ".join(P.KERNEL_NAMES[k] for k in roof.get("kernels_ms", {}))
+                               + ")",
                      "note": "path-level: 255 B x codewords / sum of the path's kernel times per step (HIP events "
                              "stamped by each kernel's dispatch, hipExtLaunchKernel); traffic = HBM bytes of the same path from rocprofv3 "
                              "FETCH_SIZE x 2 + WRITE_SIZE (tools/pmc_traffic.py); the kernels are VALU/LDS-bound, "
                              "see DESIGN.md"})
-        roof["kernels_ms"] = {P.KERNEL_NAMES[k]: v for k, v in roof["kernels_ms"].items()}
+        roof["kernels_ms"] = {P.KERNEL_NAMES[k]: v for k, v in roof.get("kernels_ms", {}).items()}
         for m in modes.values():
             if "kernels_ms" in m:
                 m["kernels_ms"] = {P.KERNEL_NAMES.get(k, k): v for k, v in m["kernels_ms"].items()}
@@ -811,6 +1049,15 @@ def main(argv=None):
             line["host_pipeline"] = host_pipeline(be, w)
         if world == 1 and not args.no_latency:
             line["single_call_latency"] = call_latency(be)
+    else:
+        if "decode_mixed" in line:
+            line["decode_mixed"].pop("_kt", None)
+            line["decode_mixed"].pop("_steps", None)
+    # every sampled codeword of every mode against the reference CPU path
+    # (after all timed loops)
+    ps = parity_sample(samples, ranks)
+    line["parity_sample"] = ps
+    line["verified"] = line["verified"] and all(v["mismatches"] == 0 for k, v in ps.items() if isinstance(v, dict))
     del w
     if not args.no_c4:
         c4 = run_strong(be, ranks, args, rank, world)

@@ -1,9 +1,9 @@
 /*
  * poporon/rng.h -- deterministic byte source (drop-in for the reference's
  * include/poporon/rng.h:14-33): xoshiro128++ seeded through splitmix32
- * (src/rng.c:17-132).  poporon_rng_next fills host memory exactly as the
- * reference does; poporon_amd_rng_fill_device (poporon_amd.h) produces the
- * same byte stream directly in device memory.
+ * (src/rng.c:17-132).  Declares exactly the reference's three functions;
+ * the device-memory variant of the same stream is an extension and lives
+ * in poporon_amd.h.
  */
 #ifndef POPORON_RNG_H
 #define POPORON_RNG_H

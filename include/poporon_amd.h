@@ -42,6 +42,13 @@ extern "C" {
 /* Message for the last failing call on this thread ("" if none). */
 const char *poporon_amd_last_error(void);
 
+/* poporon_decode (RS) writes this to *corrected_num (and the handle's
+ * last_corrected) when the call failed on the device side -- no usable GPU,
+ * or a HIP error -- rather than on the codeword: the reference never reports
+ * more than num_roots corrections, so a drop-in caller tells "device error"
+ * from "uncorrectable" (false with 0..num_roots) without a new entry point. */
+#define POPORON_AMD_DEVICE_ERROR ((size_t)-1)
+
 /* Number of HIP devices visible (0 when no GPU / no runtime). */
 int poporon_amd_device_count(void);
 

@@ -30,6 +30,8 @@ POPORON_FEC_RS = 1
 POPORON_FEC_LDPC = 2
 POPORON_FEC_BCH = 3
 POPORON_FEC_UNKNOWN = 255
+# poporon_decode's *corrected_num after a device-side failure (include/poporon_amd.h)
+DEVICE_ERROR = (1 << 64) - 1
 
 _u8p = C.POINTER(C.c_uint8)
 _u16p = C.POINTER(C.c_uint16)
@@ -282,8 +284,8 @@ class Poporon:
     def decode(self, data, parity):
         """poporon_decode on copies: returns (ok, corrected_num, data', parity').
 
-        A False result is a decode outcome (as in the reference), not an error;
-        check last_error() to tell a GPU failure apart."""
+        A False result is a decode outcome (as in the reference), not an error,
+        unless corrected_num == DEVICE_ERROR (a GPU failure; last_error() says which)."""
         d = _u8(data, copy=True)
         p = _u8(parity, copy=True)
         n = C.c_size_t(0)

@@ -1007,34 +1007,47 @@ struct KernelTimer {
         }
         rs_launch_timer = {a, b, 0};
     }
-    void done()
+    /* every call site ends a successful stage with done(true); the destructor
+     * alone runs on an early error return (HIP_OK), when a launch may have
+     * failed and never recorded its events: they go back to the pool unread */
+    void done(bool launched = true)
     {
         if (!a)
             return;
-        if (rs_launch_timer.n > 0) {
+        if (launched && rs_launch_timer.n > 0) {
             g.pending.push_back({kernel, a, b});
-        } else { /* nothing launched */
+        } else { /* nothing (successfully) launched */
             g.event_pool.push_back(a);
             g.event_pool.push_back(b);
         }
         rs_launch_timer = {nullptr, nullptr, 0};
         a = b = nullptr;
     }
-    ~KernelTimer() { done(); }
+    ~KernelTimer() { done(false); }
 };
 
+/* Folds the finished stage timings into the totals.  An entry whose events
+ * cannot be read is dropped (its events recycled) rather than left queued,
+ * so one failed launch cannot wedge every later timing call. */
 static bool drain_timing(GpuCtx &g)
 {
+    bool all = true;
     for (auto &t : g.pending) {
         float ms = 0.f;
-        HIP_OK(hipEventSynchronize(t.b));
-        HIP_OK(hipEventElapsedTime(&ms, t.a, t.b));
-        g.total_ms[t.kernel] += ms;
-        g.launches[t.kernel] += 1;
+        if (hipEventSynchronize(t.b) == hipSuccess && hipEventElapsedTime(&ms, t.a, t.b) == hipSuccess) {
+            g.total_ms[t.kernel] += ms;
+            g.launches[t.kernel] += 1;
+        } else {
+            all = false;
+        }
         g.event_pool.push_back(t.a);
         g.event_pool.push_back(t.b);
     }
     g.pending.clear();
+    if (!all) {
+        (void)hipGetLastError();
+        return fail("a timed kernel's events could not be read (launch failed?); entry dropped");
+    }
     return true;
 }
 
@@ -1931,22 +1944,15 @@ static bool bch_decode_one(poporon_t *h, uint8_t *data, size_t size, uint8_t *pa
     return true;
 }
 
-EXPORT bool poporon_decode(poporon_t *h, uint8_t *data, size_t size, uint8_t *parity, size_t *corrected_num)
+/* One RS codeword on the device: false only for a device-side failure (no
+ * usable GPU, a HIP error); the decode outcome goes to *success / *fixed. */
+static bool rs_decode_one(poporon_t *h, uint8_t *data, size_t size, uint8_t *parity, bool *success_out,
+                          size_t *fixed_out)
 {
-    if (!h || !data || !parity || !size)
-        return false;
-    if (h->fec_type == PPLN_FEC_BCH)
-        return bch_decode_one(h, data, size, parity, corrected_num);
-    if (h->fec_type != PPLN_FEC_RS)
-        return false;
     size_t fixed = 0;
     bool success = false;
-    if (!check_decode_size(h, size) || !gpu_init(h)) {
-        h->last_corrected = 0;
-        if (corrected_num)
-            *corrected_num = 0;
+    if (!gpu_init(h))
         return false;
-    }
     {
         DeviceGuard dg(h->gpu.device);
         GpuCtx &g = h->gpu;
@@ -2041,6 +2047,31 @@ EXPORT bool poporon_decode(poporon_t *h, uint8_t *data, size_t size, uint8_t *pa
                 fixed = hs[off_cor];
             }
         }
+    }
+    *success_out = success;
+    *fixed_out = fixed;
+    return true;
+}
+
+EXPORT bool poporon_decode(poporon_t *h, uint8_t *data, size_t size, uint8_t *parity, size_t *corrected_num)
+{
+    if (!h || !data || !parity || !size)
+        return false;
+    if (h->fec_type == PPLN_FEC_BCH)
+        return bch_decode_one(h, data, size, parity, corrected_num);
+    if (h->fec_type != PPLN_FEC_RS)
+        return false;
+    size_t fixed = 0;
+    bool success = false;
+    if (check_decode_size(h, size) && !rs_decode_one(h, data, size, parity, &success, &fixed)) {
+        /* no usable device / a HIP failure: not a decode outcome.  The
+         * reference never reports more than num_roots corrections, so the
+         * sentinel tells this apart from "uncorrectable" (false, count 0..32);
+         * poporon_amd_last_error() says what failed */
+        h->last_corrected = POPORON_AMD_DEVICE_ERROR;
+        if (corrected_num)
+            *corrected_num = POPORON_AMD_DEVICE_ERROR;
+        return false;
     }
     h->last_corrected = fixed;
     if (corrected_num)

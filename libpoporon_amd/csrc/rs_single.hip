@@ -193,6 +193,8 @@ struct Dec1Smem {
     uint32_t pos[32];    /* erasure slots (erasure mode) */
     uint32_t wcnt[4];    /* roots per wave (Chien) */
     uint32_t flags;
+    uint32_t low;        /* Chien: a root below the padding (its own word: a wave still
+                          * testing `flags` after the BM barrier must not see it) */
     uint32_t deg, nfix;
 };
 
@@ -230,8 +232,10 @@ __global__ __launch_bounds__(S1_WG) void rs_dec1_k(const RsDevTables *__restrict
         xs = ext[t];
     }
     s.cw[t] = (uint8_t)w;
-    if (t == 0)
+    if (t == 0) {
         s.flags = 0;
+        s.low = 0;
+    }
     if (t >= RS_NR && t < 64u)
         s.slog[t] = ZL;
     __syncthreads();
@@ -372,7 +376,7 @@ __global__ __launch_bounds__(S1_WG) void rs_dec1_k(const RsDevTables *__restrict
             if (lane == 0)
                 s.wcnt[wave] = (uint32_t)__builtin_popcountll(rb);
             if (root && (int32_t)k < pad) /* src/decode.c:132-134 */
-                atomicOr(&s.flags, F_FAIL);
+                atomicOr(&s.low, 1u);
             __syncthreads();
             uint32_t before = 0, total = 0;
 #pragma unroll
@@ -387,7 +391,7 @@ __global__ __launch_bounds__(S1_WG) void rs_dec1_k(const RsDevTables *__restrict
                     s.locs[idx] = k;
                 }
             }
-            if (total != deg && t == 0) /* src/decode.c:143-145 */
+            if ((total != deg || s.low) && t == 0) /* src/decode.c:143-145 */
                 atomicOr(&s.flags, F_FAIL);
             __syncthreads();
             if (s.flags & F_FAIL)

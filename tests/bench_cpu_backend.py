@@ -70,5 +70,21 @@ class Backend:
     def n_diff(self, a, b):
         return int((a != b).any(axis=1).sum())
 
+    def host(self, t, idx):
+        return np.asarray(t)[idx].copy()
+
+    def from_host(self, a):
+        return a.copy()
+
+    def mask_errors(self, mag, ne):
+        mag[np.arange(mag.shape[1])[None, :] >= ne[:, None]] = 0
+
+    def n_bad_mixed(self, st, ne, out, clean):
+        ok, cor = st
+        return int(((ne <= 16) & ((ok != 1) | (cor != ne) | (out != clean).any(1))).sum())
+
+    def count_ok(self, st):
+        return int(st[0].sum())
+
     def free_bytes(self):
         return 1 << 40

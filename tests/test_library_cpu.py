@@ -132,7 +132,7 @@ def test_no_gpu_fails_loudly():
     with pytest.raises(P.PoporonError, match="no CPU fallback"):
         h.encode(np.zeros(223, np.uint8))
     ok, n, _, _ = h.decode(np.zeros(223, np.uint8), np.zeros(32, np.uint8))
-    assert not ok and n == 0
+    assert not ok and n == P.DEVICE_ERROR  # a device failure, told apart from "uncorrectable" (0..32)
     assert "no CPU fallback" in P.last_error()
     with pytest.raises(P.PoporonError):
         h.encode_batch(np.zeros((4, 223), np.uint8))
