@@ -142,6 +142,11 @@ struct GpuCtx {
      * ZC_* in rs_device.h); zc_dev is its device address, NULL if unavailable */
     uint8_t *zc = nullptr, *zc_dev = nullptr;
     uint32_t zc_seq = 0; /* completion words of the single-call kernels */
+    /* the single-call server (rs_serve_k) on its own stream: srv_on while a
+     * launch may still be serving, srv_id the id of the latest launch */
+    hipStream_t sstream = nullptr;
+    bool srv_on = false;
+    uint32_t srv_id = 0;
     size_t stage_cap = 0;
     /* host-batch pipeline: PIPE_SLOTS chunks in flight, one stream each */
     struct PipeSlot {
@@ -709,7 +714,8 @@ EXPORT poporon_t *poporon_create(const poporon_config_t *config)
 static void gpu_release(GpuCtx &g)
 {
     const int dev = g.device;
-    const bool any = g.ready || g.stream || g.tab || g.gtab || g.rem || g.stage || g.hstage || g.zc || g.rem_done ||
+    const bool any = g.ready || g.stream || g.sstream || g.tab || g.gtab || g.rem || g.stage || g.hstage || g.zc ||
+                     g.rem_done ||
                      g.pipe[0].stream || g.pipe[1].stream || g.pipe[2].stream;
     if (!any || dev < 0) {
         g = GpuCtx();
@@ -737,6 +743,12 @@ static void gpu_release(GpuCtx &g)
     (void)hipFree(g.stage);
     if (g.hstage)
         (void)hipHostFree(g.hstage);
+    if (g.sstream) {
+        if (g.zc) /* ask a live server to leave now rather than at its idle limit */
+            *reinterpret_cast<volatile uint32_t *>(g.zc + ZC_STOP) = 1u;
+        (void)hipStreamSynchronize(g.sstream);
+        (void)hipStreamDestroy(g.sstream);
+    }
     if (g.zc)
         (void)hipHostFree(g.zc);
     for (auto &ps : g.pipe) {
@@ -1865,6 +1877,89 @@ static bool zc_wait(GpuCtx &g, uint32_t seq)
     }
 }
 
+/* The single-call server (rs_serve_k, rs_single.hip): a resident workgroup
+ * that polls the handle's coherent buffer, so a poporon_encode /
+ * poporon_decode call is a few posted PCIe writes and reads instead of a
+ * kernel launch.  It leaves by itself after SRV_IDLE_TICKS without a request
+ * (so a stream or device synchronisation waits at most that long for it) or
+ * SRV_MAX_TICKS in all; the next call then launches it again.
+ * POPORON_AMD_SERVE=0 turns it off (one launch per call, rs_enc1_k /
+ * rs_dec1_k). */
+#define SRV_IDLE_TICKS 100000ull  /* 1 ms of s_memrealtime (100 MHz) */
+#define SRV_MAX_TICKS 50000000ull /* 0.5 s */
+
+static bool serve_enabled()
+{
+    static const bool on = [] {
+        const char *e = getenv("POPORON_AMD_SERVE");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+
+static bool srv_launch(poporon_t *h, uint32_t last)
+{
+    GpuCtx &g = h->gpu;
+    if (!g.sstream)
+        HIP_OK(hipStreamCreateWithFlags(&g.sstream, hipStreamNonBlocking));
+    *reinterpret_cast<volatile uint32_t *>(g.zc + ZC_STOP) = 0u;
+    const uint32_t id = g.srv_id + 1u;
+    RsCorrParams prm = h->corr;
+    HIP_OK(rsk_serve(g.tab, &prm, g.zc_dev, last, id, SRV_IDLE_TICKS, SRV_MAX_TICKS, g.sstream));
+    g.srv_id = id;
+    g.srv_on = true;
+    return true;
+}
+
+/* One request through the server; the payload is in g.zc already.  A server
+ * that left before it saw the request (idle limit, lifetime) has stored its
+ * id to ZC_EXITED without serving it: launch a new one for it. */
+static bool srv_call(poporon_t *h, uint32_t op, uint32_t size, uint32_t mode)
+{
+    GpuCtx &g = h->gpu;
+    volatile uint32_t *z32 = reinterpret_cast<volatile uint32_t *>(g.zc);
+    z32[ZC_OP / 4] = op;
+    z32[ZC_SIZE / 4] = size;
+    z32[ZC_MODE / 4] = mode;
+    const uint32_t seq = ++g.zc_seq;
+    std::atomic_thread_fence(std::memory_order_release); /* the payload and header before the request word */
+    z32[ZC_REQ / 4] = seq;
+    if (!g.srv_on && !srv_launch(h, seq - 1u))
+        return false;
+    const volatile uint32_t *f = z32 + ZC_FLAG / 4, *ex = z32 + ZC_EXITED / 4;
+    for (uint32_t spin = 1;; ++spin) {
+        if (*f == seq) {
+            std::atomic_thread_fence(std::memory_order_acquire);
+            return true;
+        }
+        if (*ex == g.srv_id) { /* the server has left */
+            std::atomic_thread_fence(std::memory_order_acquire);
+            if (*f == seq) {
+                std::atomic_thread_fence(std::memory_order_acquire);
+                return true;
+            }
+            g.srv_on = false;
+            if (!srv_launch(h, seq - 1u))
+                return false;
+            continue;
+        }
+        if ((spin & 4095u) == 0u) {
+            const hipError_t e = hipStreamQuery(g.sstream);
+            if (e == hipSuccess && *ex != g.srv_id && *f != seq) {
+                g.srv_on = false;
+                return fail("single-call server ended without serving or leaving its exit word");
+            }
+            if (e != hipSuccess && e != hipErrorNotReady) {
+                g.srv_on = false;
+                return fail("HIP error %d (%s) in the single-call server", (int)e, hipGetErrorString(e));
+            }
+        }
+#if defined(__x86_64__)
+        __builtin_ia32_pause();
+#endif
+    }
+}
+
 EXPORT bool poporon_encode(poporon_t *h, uint8_t *data, size_t size, uint8_t *parity)
 {
     if (!h || !data || !parity)
@@ -1885,13 +1980,18 @@ EXPORT bool poporon_encode(poporon_t *h, uint8_t *data, size_t size, uint8_t *pa
      * launch, no copies, no stream synchronisation) */
     if (h->fec_type == PPLN_FEC_RS && h->fast && size >= 1 && size <= 223 && ensure_zc(g)) {
         memcpy(g.zc + ZC_DATA, data, size);
-        const uint32_t seq = ++g.zc_seq;
-        KernelTimer t(g, POPORON_AMD_KERNEL_ENCODE, g.stream);
-        HIP_OK(rsk_encode1(g.tab, g.zc_dev + ZC_DATA, g.zc_dev + ZC_PAR, (uint32_t)size,
-                           reinterpret_cast<uint32_t *>(g.zc_dev + ZC_FLAG), seq, g.stream));
-        t.done();
-        if (!zc_wait(g, seq))
-            return false;
+        if (serve_enabled() && !g.timing) {
+            if (!srv_call(h, RS_SRV_ENCODE, (uint32_t)size, 0u))
+                return false;
+        } else {
+            const uint32_t seq = ++g.zc_seq;
+            KernelTimer t(g, POPORON_AMD_KERNEL_ENCODE, g.stream);
+            HIP_OK(rsk_encode1(g.tab, g.zc_dev + ZC_DATA, g.zc_dev + ZC_PAR, (uint32_t)size,
+                               reinterpret_cast<uint32_t *>(g.zc_dev + ZC_FLAG), seq, g.stream));
+            t.done();
+            if (!zc_wait(g, seq))
+                return false;
+        }
         memcpy(parity, g.zc + ZC_PAR, nr);
         return true;
     }
@@ -1985,15 +2085,20 @@ static bool rs_decode_one(poporon_t *h, uint8_t *data, size_t size, uint8_t *par
             prm.size = (uint32_t)size;
             prm.pad = (int32_t)(h->rs->gf->field_size - h->rs->num_roots - size);
             uint8_t *zd = g.zc_dev;
-            const uint32_t seq = ++g.zc_seq;
-            KernelTimer t(g, POPORON_AMD_KERNEL_SINGLE, g.stream);
-            HIP_OK(rsk_decode1(g.tab, &prm, mode, zd + ZC_DATA, zd + ZC_PAR, nullptr,
-                               reinterpret_cast<const uint32_t *>(zd + ZC_POS), zd + ZC_CNT, 4u,
-                               reinterpret_cast<const uint16_t *>(zd + ZC_EXT), zd + ZC_OK, zd + ZC_COR,
-                               reinterpret_cast<uint32_t *>(zd + ZC_FLAG), seq, g.stream));
-            t.done();
-            if (!zc_wait(g, seq))
-                return false;
+            if (serve_enabled() && !g.timing && size == prm.size && prm.pad == (int32_t)(RS_NN - RS_NR - size)) {
+                if (!srv_call(h, RS_SRV_DECODE, (uint32_t)size, mode))
+                    return false;
+            } else {
+                const uint32_t seq = ++g.zc_seq;
+                KernelTimer t(g, POPORON_AMD_KERNEL_SINGLE, g.stream);
+                HIP_OK(rsk_decode1(g.tab, &prm, mode, zd + ZC_DATA, zd + ZC_PAR, nullptr,
+                                   reinterpret_cast<const uint32_t *>(zd + ZC_POS), zd + ZC_CNT, 4u,
+                                   reinterpret_cast<const uint16_t *>(zd + ZC_EXT), zd + ZC_OK, zd + ZC_COR,
+                                   reinterpret_cast<uint32_t *>(zd + ZC_FLAG), seq, g.stream));
+                t.done();
+                if (!zc_wait(g, seq))
+                    return false;
+            }
             memcpy(data, z + ZC_DATA, size);
             memcpy(parity, z + ZC_PAR, nr);
             success = z[ZC_OK] != 0;

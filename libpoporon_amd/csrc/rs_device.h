@@ -181,6 +181,13 @@ hipError_t rsk_decode1(const RsDevTables *tab, const RsCorrParams *prm, uint32_t
                        uint32_t cnt_bytes, const uint16_t *ext, uint8_t *ok, uint8_t *corrected, uint32_t *flag,
                        uint32_t seq, hipStream_t stream);
 
+/* The single-call server: one resident workgroup serving poporon_encode /
+ * poporon_decode requests posted in the coherent host buffer (rs_single.hip
+ * rs_serve_k); it leaves after idle_ticks (100 MHz) without a request or
+ * max_ticks in all, storing `id` to ZC_EXITED. */
+hipError_t rsk_serve(const RsDevTables *tab, const RsCorrParams *prm, uint8_t *zc_dev, uint32_t last, uint32_t id,
+                     uint64_t idle_ticks, uint64_t max_ticks, hipStream_t stream);
+
 /* layout of the coherent host buffer of the single-call API (GpuCtx::zc) */
 #define ZC_DATA 0    /* message / data bytes (<= 223) */
 #define ZC_PAR 256   /* 32 parity bytes */
@@ -190,7 +197,17 @@ hipError_t rsk_decode1(const RsDevTables *tab, const RsCorrParams *prm, uint32_t
 #define ZC_OK 576
 #define ZC_COR 577
 #define ZC_FLAG 640  /* u32 completion word */
+/* the single-call server (rs_serve_k): request header written by the host
+ * (ZC_REQ last, its own 64-byte line), the server's exit word, the stop word */
+#define ZC_REQ 704   /* u32 request sequence number */
+#define ZC_OP 708    /* u32 RS_SRV_ENCODE / RS_SRV_DECODE */
+#define ZC_SIZE 712  /* u32 message bytes (1..223) */
+#define ZC_MODE 716  /* u32 decode mode (rsk_decode1) */
+#define ZC_EXITED 768 /* u32: the id of the last server launch that has left */
+#define ZC_STOP 832  /* u32: nonzero asks the server to leave */
 #define ZC_BYTES 1024
+#define RS_SRV_ENCODE 1u
+#define RS_SRV_DECODE 2u
 
 /* poly syndromes (32 B per codeword, rsk_syndrome) -> log form: out[c*stride + i]
  * = log S_i (255 = zero), flag[c] = any S_i nonzero; out / flag may be NULL */

@@ -125,13 +125,12 @@ __device__ __forceinline__ void fill_tabs(Tabs &s, const RsDevTables *__restrict
  * row (two 16-byte loads, issued with the message and table loads: one
  * memory round trip); the products are XOR-reduced over each wave (DPP),
  * then over the four waves in LDS. */
-__global__ __launch_bounds__(S1_WG) void rs_enc1_k(const RsDevTables *__restrict__ T, const uint8_t *data,
-                                                   uint8_t *parity, uint32_t size, uint32_t *flag, uint32_t seq)
+/* the encode of one message by the whole workgroup; the tables in s are
+ * filled (or being filled: the first barrier below orders them) */
+__device__ __forceinline__ void enc1_body(Tabs &s, uint32_t (*wred)[8], const RsDevTables *__restrict__ T,
+                                          const uint8_t *data, uint8_t *parity, uint32_t size)
 {
-    __shared__ Tabs s;
-    __shared__ uint32_t wred[4][8];
     const uint32_t t = threadIdx.x, lane = t & 63u, wave = t >> 6;
-    fill_tabs(s, T, t);
     uint32_t w = 0;
     uint4 q0 = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu), q1 = q0;
     if (t < size) {
@@ -169,6 +168,16 @@ __global__ __launch_bounds__(S1_WG) void rs_enc1_k(const RsDevTables *__restrict
         const uint32_t d = wred[0][t >> 2] ^ wred[1][t >> 2] ^ wred[2][t >> 2] ^ wred[3][t >> 2];
         parity[t] = (uint8_t)(d >> (8u * (t & 3u)));
     }
+}
+
+__global__ __launch_bounds__(S1_WG) void rs_enc1_k(const RsDevTables *__restrict__ T, const uint8_t *data,
+                                                   uint8_t *parity, uint32_t size, uint32_t *flag, uint32_t seq)
+{
+    __shared__ Tabs s;
+    __shared__ uint32_t wred[4][8];
+    const uint32_t t = threadIdx.x;
+    fill_tabs(s, T, t);
+    enc1_body(s, wred, T, data, parity, size);
     if (flag) {
         __syncthreads(); /* every parity store issued before the flag */
         if (t == 0)
@@ -204,22 +213,21 @@ struct Dec1Smem {
 /* mode: 0 plain, 1 erasure (pos8 or pos32 slots, *cnt erasures), 2 external
  * log-form syndromes (ext, 32 x u16).  ok / cor: one byte each (written
  * always, as rs_decode writes corrected_num also on failure). */
-__global__ __launch_bounds__(S1_WG) void rs_dec1_k(const RsDevTables *__restrict__ T, RsCorrParams P, uint32_t mode,
-                                                   uint8_t *data, uint8_t *parity, const uint8_t *pos8,
-                                                   const uint32_t *pos32, const void *cnt, uint32_t cnt_bytes,
-                                                   const uint16_t *ext, uint8_t *okp, uint8_t *corp,
-                                                   uint32_t *flag, uint32_t seq)
+/* rs_decode of one codeword by the whole workgroup (the tables in s.g
+ * filled, or being filled: the first barrier orders them); ok / corrected
+ * stored, the caller signals completion */
+__device__ void dec1_body(Dec1Smem &s, const RsCorrParams &P, uint32_t mode, uint8_t *data, uint8_t *parity,
+                          const uint8_t *pos8, const uint32_t *pos32, const void *cnt, uint32_t cnt_bytes,
+                          const uint16_t *ext, uint8_t *okp, uint8_t *corp)
 {
-    __shared__ Dec1Smem s;
     const uint32_t t = threadIdx.x, lane = t & 63u, wave = t >> 6;
     const uint32_t size = P.size, L = size + RS_NR;
     const int32_t pad = P.pad;
     uint32_t ok = 0, fixed = 0;
     /* STAMP 0 */
 
-    /* ---- inputs: tables, the codeword (one byte per thread), slots: all
-     * loads issued together (the codeword may be host memory) ---- */
-    fill_tabs(s.g, T, t);
+    /* ---- inputs: the codeword (one byte per thread), slots: all loads
+     * issued together (the codeword may be host memory) ---- */
     uint32_t w = 0;
     if (t < L)
         w = t < size ? data[t] : parity[t - size];
@@ -543,6 +551,18 @@ finish:
         *okp = (uint8_t)ok;
         *corp = (uint8_t)fixed;
     }
+}
+
+__global__ __launch_bounds__(S1_WG) void rs_dec1_k(const RsDevTables *__restrict__ T, RsCorrParams P, uint32_t mode,
+                                                   uint8_t *data, uint8_t *parity, const uint8_t *pos8,
+                                                   const uint32_t *pos32, const void *cnt, uint32_t cnt_bytes,
+                                                   const uint16_t *ext, uint8_t *okp, uint8_t *corp,
+                                                   uint32_t *flag, uint32_t seq)
+{
+    __shared__ Dec1Smem s;
+    const uint32_t t = threadIdx.x;
+    fill_tabs(s.g, T, t);
+    dec1_body(s, P, mode, data, parity, pos8, pos32, cnt, cnt_bytes, ext, okp, corp);
     if (flag) {
         __syncthreads(); /* every result store issued before the flag */
         if (t == 0)
@@ -568,5 +588,95 @@ extern "C" hipError_t rsk_decode1(const RsDevTables *tab, const RsCorrParams *pr
 {
     RS_LAUNCH(rs_dec1_k, dim3(1), dim3(S1_WG), 0, stream, tab, *prm, mode, data, parity, pos8, pos32, cnt,
                        cnt_bytes, ext, ok, corrected, flag, seq);
+    return hipGetLastError();
+}
+
+/* ------------------------------------------------------------------------ */
+/* single-call server                                                        */
+/* ------------------------------------------------------------------------ */
+
+/*
+ * rs_serve_k: one workgroup that stays resident between single-codeword calls
+ * and serves them from the handle's coherent host buffer (ZC_* layout,
+ * rs_device.h), so that a poporon_encode / poporon_decode call costs no kernel
+ * launch: the host writes the codeword and a request header there and bumps
+ * ZC_REQ; lane 0 polls ZC_REQ (system-scope acquire loads over PCIe), the
+ * workgroup runs enc1_body / dec1_body on the buffer and stores the request's
+ * sequence number to ZC_FLAG with a system-scope release after every result.
+ * The tables are filled once per launch.
+ *
+ * Every launch ends on its own: after idle_ticks of s_memrealtime (100 MHz)
+ * without a request, after max_ticks in all, or when the host sets ZC_STOP
+ * (poporon_destroy).  It then stores its launch id to ZC_EXITED and serves
+ * nothing more; a request the host posted meanwhile is seen unserved there
+ * and the host launches a new server for it (api.cpp srv_call), on the same
+ * stream, so two servers never run at once.
+ */
+__global__ __launch_bounds__(S1_WG) void rs_serve_k(const RsDevTables *__restrict__ T, RsCorrParams P, uint8_t *zc,
+                                                    uint32_t last, uint32_t id, uint64_t idle_ticks,
+                                                    uint64_t max_ticks)
+{
+    __shared__ Dec1Smem s;
+    __shared__ uint32_t cmd[4]; /* seq, op (0: leave), size, mode */
+    const uint32_t t = threadIdx.x;
+    fill_tabs(s.g, T, t);
+    uint32_t *req = reinterpret_cast<uint32_t *>(zc + ZC_REQ);
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    uint64_t idle0 = t0;
+    for (;;) {
+        if (t == 0) {
+            uint32_t r = last, op = 0;
+            for (;;) {
+                r = __hip_atomic_load(req, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+                if (r != last) {
+                    op = __hip_atomic_load(reinterpret_cast<uint32_t *>(zc + ZC_OP), __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_SYSTEM);
+                    cmd[2] = __hip_atomic_load(reinterpret_cast<uint32_t *>(zc + ZC_SIZE), __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_SYSTEM);
+                    cmd[3] = __hip_atomic_load(reinterpret_cast<uint32_t *>(zc + ZC_MODE), __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_SYSTEM);
+                    break;
+                }
+                const uint32_t stop = __hip_atomic_load(reinterpret_cast<uint32_t *>(zc + ZC_STOP), __ATOMIC_RELAXED,
+                                                        __HIP_MEMORY_SCOPE_SYSTEM);
+                const uint64_t now = __builtin_amdgcn_s_memrealtime();
+                if (stop || now - idle0 > idle_ticks || now - t0 > max_ticks)
+                    break; /* op = 0: leave */
+                __builtin_amdgcn_s_sleep(1);
+            }
+            cmd[0] = r;
+            cmd[1] = op;
+        }
+        __syncthreads();
+        const uint32_t seq = cmd[0], op = cmd[1], size = cmd[2], mode = cmd[3];
+        if (op == 0u || size == 0u || size > 223u)
+            break; /* uniform (a malformed request also ends the launch: the host sees it unserved) */
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, ""); /* this wave's loads of the payload: after the request */
+        if (op == RS_SRV_ENCODE) {
+            enc1_body(s.g, reinterpret_cast<uint32_t(*)[8]>(s.part), T, zc + ZC_DATA, zc + ZC_PAR, size);
+        } else {
+            RsCorrParams Q = P;
+            Q.size = size;
+            Q.pad = (int32_t)(RS_NN - RS_NR - size);
+            dec1_body(s, Q, mode, zc + ZC_DATA, zc + ZC_PAR, nullptr, reinterpret_cast<const uint32_t *>(zc + ZC_POS),
+                      zc + ZC_CNT, 4u, reinterpret_cast<const uint16_t *>(zc + ZC_EXT), zc + ZC_OK, zc + ZC_COR);
+        }
+        __syncthreads(); /* every result store issued before the completion word */
+        if (t == 0)
+            __hip_atomic_store(reinterpret_cast<uint32_t *>(zc + ZC_FLAG), seq, __ATOMIC_RELEASE,
+                               __HIP_MEMORY_SCOPE_SYSTEM);
+        last = seq;
+        idle0 = __builtin_amdgcn_s_memrealtime();
+    }
+    if (t == 0)
+        __hip_atomic_store(reinterpret_cast<uint32_t *>(zc + ZC_EXITED), id, __ATOMIC_RELEASE,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+extern "C" hipError_t rsk_serve(const RsDevTables *tab, const RsCorrParams *prm, uint8_t *zc_dev, uint32_t last,
+                                uint32_t id, uint64_t idle_ticks, uint64_t max_ticks, hipStream_t stream)
+{
+    hipLaunchKernelGGL(rs_serve_k, dim3(1), dim3(S1_WG), 0, stream, tab, *prm, zc_dev, last, id, idle_ticks,
+                       max_ticks);
     return hipGetLastError();
 }

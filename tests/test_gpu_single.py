@@ -184,3 +184,34 @@ def test_single_call_many(oracle_default):
         cw[rng.permutation(255)[:16]] ^= rng.integers(1, 256, 16, dtype=np.uint8)
         ok, n, d, q = h.decode(cw[:223], cw[223:])
         assert ok and n == 16 and (d == msgs[c]).all() and (q == p).all(), c
+
+
+def test_single_call_server_idle_and_relaunch(oracle_default):
+    """The single-call server (rs_serve_k) leaves after 1 ms without a
+    request and is launched again by the next call; calls spaced around that
+    limit, device batches and device synchronisations in between, and a
+    second handle serving at the same time all give the oracle's bytes."""
+    import time
+
+    import torch
+    _need_gpu()
+    h, h2 = P.Poporon.default(), P.Poporon.default()
+    rng = np.random.default_rng(2024)
+    msgs = rng.integers(0, 256, (48, 223), dtype=np.uint8)
+    want = oracle_default.encode_batch(msgs)
+    for c in range(48):
+        if c % 3 == 0:
+            time.sleep([0.0, 0.0009, 0.0011, 0.003][(c // 3) % 4])  # around the 1 ms idle limit
+        if c % 8 == 5:
+            torch.cuda.synchronize()  # waits for a live server to leave (at most its idle limit)
+        if c % 8 == 6:
+            got = h.decode_batch(np.tile(msgs[c], (3, 1)), np.tile(want[c], (3, 1)))  # a device batch between calls
+            assert got[0].all()
+        hh = h if c % 2 else h2
+        assert (hh.encode(msgs[c]) == want[c]).all(), c
+        cw = np.concatenate([msgs[c], want[c]])
+        cw[rng.permutation(255)[:16]] ^= rng.integers(1, 256, 16, dtype=np.uint8)
+        ok, n, d, q = hh.decode(cw[:223], cw[223:])
+        assert ok and n == 16 and (d == msgs[c]).all() and (q == want[c]).all(), c
+    h.close()  # asks a live server to leave at once
+    assert (h2.encode(msgs[0]) == want[0]).all()
