@@ -1918,34 +1918,35 @@ static bool srv_call(poporon_t *h, uint32_t op, uint32_t size, uint32_t mode)
 {
     GpuCtx &g = h->gpu;
     volatile uint32_t *z32 = reinterpret_cast<volatile uint32_t *>(g.zc);
-    z32[ZC_OP / 4] = op;
-    z32[ZC_SIZE / 4] = size;
-    z32[ZC_MODE / 4] = mode;
     const uint32_t seq = ++g.zc_seq;
-    std::atomic_thread_fence(std::memory_order_release); /* the payload and header before the request word */
-    z32[ZC_REQ / 4] = seq;
-    if (!g.srv_on && !srv_launch(h, seq - 1u))
+    /* the request word differs from the last one the server served (their
+     * sequence numbers differ: 14 bits, one request in flight at a time) */
+    const uint32_t prev = z32[ZC_REQ / 4], word = ZC_REQ_WORD(seq, op, size, mode);
+    z32[ZC_FLAG / 4] = 0u; /* the server answers with the request word (never 0: op >= 1) */
+    std::atomic_thread_fence(std::memory_order_release); /* the payload before the request word */
+    z32[ZC_REQ / 4] = word;
+    if (!g.srv_on && !srv_launch(h, prev))
         return false;
     const volatile uint32_t *f = z32 + ZC_FLAG / 4, *ex = z32 + ZC_EXITED / 4;
     for (uint32_t spin = 1;; ++spin) {
-        if (*f == seq) {
+        if (*f == word) {
             std::atomic_thread_fence(std::memory_order_acquire);
             return true;
         }
         if (*ex == g.srv_id) { /* the server has left */
             std::atomic_thread_fence(std::memory_order_acquire);
-            if (*f == seq) {
+            if (*f == word) {
                 std::atomic_thread_fence(std::memory_order_acquire);
                 return true;
             }
             g.srv_on = false;
-            if (!srv_launch(h, seq - 1u))
+            if (!srv_launch(h, prev))
                 return false;
             continue;
         }
         if ((spin & 4095u) == 0u) {
             const hipError_t e = hipStreamQuery(g.sstream);
-            if (e == hipSuccess && *ex != g.srv_id && *f != seq) {
+            if (e == hipSuccess && *ex != g.srv_id && *f != word) {
                 g.srv_on = false;
                 return fail("single-call server ended without serving or leaving its exit word");
             }

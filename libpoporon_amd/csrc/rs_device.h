@@ -199,10 +199,12 @@ hipError_t rsk_serve(const RsDevTables *tab, const RsCorrParams *prm, uint8_t *z
 #define ZC_FLAG 640  /* u32 completion word */
 /* the single-call server (rs_serve_k): request header written by the host
  * (ZC_REQ last, its own 64-byte line), the server's exit word, the stop word */
-#define ZC_REQ 704   /* u32 request sequence number */
-#define ZC_OP 708    /* u32 RS_SRV_ENCODE / RS_SRV_DECODE */
-#define ZC_SIZE 712  /* u32 message bytes (1..223) */
-#define ZC_MODE 716  /* u32 decode mode (rsk_decode1) */
+#define ZC_REQ 704   /* u32 request word: ZC_REQ_WORD(seq, op, size, mode) */
+#define ZC_REQ_WORD(seq, op, size, mode) \
+    ((((seq) & 0x3FFFu) << 18) | (((mode) & 3u) << 10) | (((op) & 3u) << 8) | ((size) & 0xFFu))
+#define ZC_REQ_OP(w) (((w) >> 8) & 3u)    /* RS_SRV_ENCODE / RS_SRV_DECODE */
+#define ZC_REQ_MODE(w) (((w) >> 10) & 3u) /* decode mode (rsk_decode1) */
+#define ZC_REQ_SIZE(w) ((w) & 0xFFu)      /* message bytes (1..223) */
 #define ZC_EXITED 768 /* u32: the id of the last server launch that has left */
 #define ZC_STOP 832  /* u32: nonzero asks the server to leave */
 #define ZC_BYTES 1024

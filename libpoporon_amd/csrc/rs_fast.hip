@@ -891,7 +891,11 @@ __global__ __launch_bounds__(EWG, ERA_WAVES) void rs_era_k(const RsDevTables *__
  * in (ds_xor_b32), and the block is written back the same way -- 2 x 16 memory
  * requests per wave-instruction row instead of one request per corrected
  * byte (scattered byte read-modify-writes measured 0.15 ms per 2^20
- * codewords with 16 errors, bound by the L2's request rate).  Other layouts
+ * codewords with 16 errors, bound by the L2's request rate).  The block's
+ * loads and stores are non-temporal: the codewords are not read again by
+ * this decode, and the dirty lines written back here rather than evicted by
+ * the next kernel's stream measured the following encode 0.100 vs 0.109 ms
+ * and the round trip +2 % (profiles/r03_apply_nt_ab.log).  Other layouts
  * and a batch's last partial wave correct byte by byte.  Locations are
  * distinct (distinct roots), so the order of the corrections is immaterial.
  */
@@ -937,8 +941,10 @@ __global__ __launch_bounds__(AWG) void rs_apply_k(const uint8_t *__restrict__ me
 #pragma unroll
         for (uint32_t k = 0; k < 16; ++k) {
             const uint32_t c = lane + 64u * k;
-            if (c < ABLK)
-                im[c] = src[c];
+            if (c < ABLK) {
+                const lds_u32x4_t v = __builtin_nontemporal_load(reinterpret_cast<const lds_u32x4_t *>(src + c));
+                im[c] = make_uint4(v.x, v.y, v.z, v.w);
+            }
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
@@ -959,8 +965,10 @@ __global__ __launch_bounds__(AWG) void rs_apply_k(const uint8_t *__restrict__ me
 #pragma unroll
         for (uint32_t k = 0; k < 16; ++k) {
             const uint32_t c = lane + 64u * k;
-            if (c < ABLK)
-                dst[c] = im[c];
+            if (c < ABLK) {
+                const uint4 v = im[c];
+                __builtin_nontemporal_store(lds_u32x4_t{v.x, v.y, v.z, v.w}, reinterpret_cast<lds_u32x4_t *>(dst + c));
+            }
         }
     } else if (fast) {
         uint8_t *cdata = data + cw * dstride, *cpar = parity + cw * pstride;

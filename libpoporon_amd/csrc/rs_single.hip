@@ -627,14 +627,12 @@ __global__ __launch_bounds__(S1_WG) void rs_serve_k(const RsDevTables *__restric
         if (t == 0) {
             uint32_t r = last, op = 0;
             for (;;) {
+                /* one PCIe round trip per poll: the whole request is this word */
                 r = __hip_atomic_load(req, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
                 if (r != last) {
-                    op = __hip_atomic_load(reinterpret_cast<uint32_t *>(zc + ZC_OP), __ATOMIC_RELAXED,
-                                           __HIP_MEMORY_SCOPE_SYSTEM);
-                    cmd[2] = __hip_atomic_load(reinterpret_cast<uint32_t *>(zc + ZC_SIZE), __ATOMIC_RELAXED,
-                                               __HIP_MEMORY_SCOPE_SYSTEM);
-                    cmd[3] = __hip_atomic_load(reinterpret_cast<uint32_t *>(zc + ZC_MODE), __ATOMIC_RELAXED,
-                                               __HIP_MEMORY_SCOPE_SYSTEM);
+                    op = ZC_REQ_OP(r);
+                    cmd[2] = ZC_REQ_SIZE(r);
+                    cmd[3] = ZC_REQ_MODE(r);
                     break;
                 }
                 const uint32_t stop = __hip_atomic_load(reinterpret_cast<uint32_t *>(zc + ZC_STOP), __ATOMIC_RELAXED,
