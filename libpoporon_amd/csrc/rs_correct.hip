@@ -698,10 +698,15 @@ __global__ __launch_bounds__(COR_WG) void rs_correct_k(const RsDevTables *__rest
                                                        uint8_t *__restrict__ meta = nullptr)
 {
     /* list mode (the split decode's fallback, rs_fast.hip): the codewords
-     * list[0 .. *list_n); otherwise 0 .. count - 1.  Blocks with no work
-     * leave before filling the tables. */
+     * list[0 .. *list_n); otherwise 0 .. count - 1.  The codewords are dealt
+     * to the waves in runs of 64, run c to workgroup c mod G, so that a short
+     * list (or a small batch) spreads over every CU instead of filling the
+     * first few workgroups: each wave is one lane-serial decode chain, and
+     * the time of a short list is the latency of the busiest SIMD's waves
+     * (74k beyond-capacity codewords of 2^20 on 73 of 256 CUs took 0.36 ms).
+     * Blocks with no work leave before filling the tables. */
     const size_t n = list ? (size_t)*list_n : count;
-    if ((size_t)blockIdx.x * COR_WG >= n)
+    if ((size_t)blockIdx.x * 64u >= n)
         return;
     /* one block, carved by hand: the layout (and lgf ending exactly at the
      * allocation's end) is part of the arithmetic, see the header */
@@ -737,8 +742,9 @@ __global__ __launch_bounds__(COR_WG) void rs_correct_k(const RsDevTables *__rest
      * correction when any of its codewords needs it (the rest, with zero
      * syndromes, ride through BM as no-ops and leave at deg = 0): the BM
      * bounds are then full-wave DPP reductions. */
-    for (size_t base = (size_t)blockIdx.x * COR_WG; base < n; base += (size_t)gridDim.x * COR_WG) {
-        const size_t idx = base + threadIdx.x;
+    const uint32_t wslot = threadIdx.x >> 6, lane = threadIdx.x & 63u;
+    for (size_t run = (size_t)wslot * gridDim.x + blockIdx.x; run * 64u < n; run += (size_t)(COR_WG / 64) * gridDim.x) {
+        const size_t idx = run * 64u + lane; /* the wave's run of 64 codewords: the trip count is wave-uniform */
         const bool valid = idx < n;
         const size_t cw = list ? (valid ? (size_t)list[idx] : 0) : idx;
         uint32_t sw[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -796,9 +802,12 @@ __global__ __launch_bounds__(COR_WG) void rs_correct_k(const RsDevTables *__rest
     }
 }
 
+/* one workgroup per CU at most, and no more than there are runs of 64
+ * codewords to deal (a small batch still spreads over the CUs) */
 static int persistent_grid(size_t count, int wg, int num_cu)
 {
-    size_t need = (count + wg - 1) / wg;
+    (void)wg;
+    size_t need = (count + 63) / 64;
     size_t g = (size_t)(num_cu > 0 ? num_cu : 256);
     return (int)(need < g ? (need ? need : 1) : g);
 }

@@ -26,6 +26,8 @@ for step in "$@"; do
     tests) run tests 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread ;;
     tests_all) run tests_all 900 python -m pytest tests -m gpu -q ;;
     bench) run bench 600 python bench.py ;;
+    lat) run lat 200 python tools/lat_single.py 2000
+         POPORON_AMD_SERVE=0 run lat_noserve 200 python tools/lat_single.py 2000 ;;
     prof) run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- \
         python3 bench.py --no-cpu-baseline --no-host --no-c4 --no-latency --steps 10 ;;
     pmc)
