@@ -349,10 +349,14 @@ def shard(total, rank, world):
 
 
 def run_strong(be, ranks, args, rank, world):
+    import numpy as np
     lo, hi = shard(args.c4_total, rank, world)
     t_codec, nbad, csum_in, csum_out = 0.0, 0, 0, 0
     chunk = max(1, args.c4_chunk)
     reps = max(1, args.c4_reps)
+    # parity sample: every C4_SAMPLE_STRIDE-th global codeword of the first
+    # repetition (its encode and its decode), checked after the timed loops
+    senc, sdec = {"msg": [], "got_par": []}, {"in": [], "out": [], "ok": [], "cor": []}
     for rep in range(reps):
         t_rep = 0.0
         for a in range(lo, hi, chunk):
@@ -364,12 +368,18 @@ def run_strong(be, ranks, args, rank, world):
             be.encode(buf)
             be.sync()
             t_rep += time.perf_counter() - t0
+            idx = np.arange((-a) % C4_SAMPLE_STRIDE, n, C4_SAMPLE_STRIDE, dtype=np.int64)
             if rep == 0:
                 csum_in = (csum_in + be.checksum(buf, a)) & M64
+                rows = be.host(buf, idx)
+                senc["msg"].append(rows[:, :K])
+                senc["got_par"].append(rows[:, K:])
             err = be.errors(a, n, 16, N, SEED + 5)
             be.channel(buf, err)
             del err
             st = be.status(n)
+            if rep == 0:
+                sdec["in"].append(be.host(buf, idx))
             be.sync()
             t0 = time.perf_counter()
             be.decode(buf, st)
@@ -378,6 +388,9 @@ def run_strong(be, ranks, args, rank, world):
             if rep == 0:
                 nbad += be.n_bad(st, 16)
                 csum_out = (csum_out + be.checksum(buf, a)) & M64
+                sdec["out"].append(be.host(buf, idx))
+                sdec["ok"].append(be.host(st[0], idx))
+                sdec["cor"].append(be.host(st[1], idx))
             del buf, st
         t_codec = t_rep if rep == 0 else min(t_codec, t_rep)
     t = ranks.max(t_codec)
@@ -390,7 +403,9 @@ def run_strong(be, ranks, args, rank, world):
             "timed": f"encode + decode@16 of each rank's range (best of {reps}), max over ranks; "
                      "synthesis, channel and checksums untimed",
             "verified": nbad == 0 and cs_in == cs_out,
-            "parity_checksum": cs_out}
+            "parity_checksum": cs_out,
+            "_samples": {"configs4_encode": {k: np.concatenate(v) for k, v in senc.items()},
+                         "configs4_decode16": {k: np.concatenate(v) for k, v in sdec.items()}}}
 
 
 # ----------------------------------------------------------------------------
@@ -643,6 +658,7 @@ def run_mixed(be, ranks, args, rank, world, w):
 # parity sample against the reference CPU path (SURVEY 8(d) "GPU timing")
 # ----------------------------------------------------------------------------
 SAMPLE_STRIDE = 4096
+C4_SAMPLE_STRIDE = 65536  # configs[4]: 1,024 of the 2^26 codewords, whatever the split
 
 
 def sample_index(B):
@@ -784,7 +800,10 @@ def host_pipeline(be, w, reps=3):
 def call_latency(be, calls=2000):
     """The reference's calling pattern: one codeword per poporon_encode /
     poporon_decode call (include/poporon.h:90-91), host buffers, on the GPU
-    (one H2D copy, the kernels, one D2H copy per call)."""
+    (the single-call server rs_serve_k).  Timed by a C loop through the
+    library's own entry points (testutil ptu_time_encode / ptu_time_decode),
+    as the CPU baseline's C loop times the reference; the same calls made
+    one by one from Python through ctypes are reported beside it."""
     import ctypes as C
 
     import numpy as np
@@ -794,26 +813,35 @@ def call_latency(be, calls=2000):
     lib = rs.lib
     msgs = T.synth_rows_cpu(SEED + 7, 0, calls, K)
     pos, mag = T.synth_errors_cpu(SEED + 8, 0, calls, 16, N)
-    par = np.zeros((calls, NR), np.uint8)
     vp = lambda a: a.ctypes.data_as(C.c_void_p)  # noqa: E731
-    for c in range(16):  # warm-up (staging allocation, kernel load)
+    par = np.zeros((calls, NR), np.uint8)
+    for c in range(16):  # warm-up (staging allocation, the server's first launch)
         lib.poporon_encode(rs.h, vp(msgs[c]), K, vp(par[c]))
-    t0 = time.perf_counter()
-    for c in range(calls):
-        lib.poporon_encode(rs.h, vp(msgs[c]), K, vp(par[c]))
-    te = time.perf_counter() - t0
+    te = T.time_encode(lib, rs.h, msgs, par)
     cw = T.channel_xor_cpu(np.concatenate([msgs, par], 1), pos, mag)
     d, p = np.ascontiguousarray(cw[:, :K]), np.ascontiguousarray(cw[:, K:])
+    td, ok, cor = T.time_decode(lib, rs.h, d, p)
+    assert te > 0 and ok.all() and (cor == 16).all() and (d == msgs).all()
+    # the same through ctypes, one Python call each
+    par2 = np.zeros((calls, NR), np.uint8)
+    t0 = time.perf_counter()
+    for c in range(calls):
+        lib.poporon_encode(rs.h, vp(msgs[c]), K, vp(par2[c]))
+    tpe = time.perf_counter() - t0
+    d2, p2 = np.ascontiguousarray(cw[:, :K]), np.ascontiguousarray(cw[:, K:])
     n = C.c_size_t(0)
     fixed = 0
     t0 = time.perf_counter()
     for c in range(calls):
-        fixed += bool(lib.poporon_decode(rs.h, vp(d[c]), K, vp(p[c]), C.byref(n))) and n.value == 16
-    td = time.perf_counter() - t0
-    assert fixed == calls and (d == msgs).all()
+        fixed += bool(lib.poporon_decode(rs.h, vp(d2[c]), K, vp(p2[c]), C.byref(n))) and n.value == 16
+    tpd = time.perf_counter() - t0
+    assert (par2 == par).all() and fixed == calls and (d2 == msgs).all()
     return {"encode_us_per_call": round(te / calls * 1e6, 2), "decode16_us_per_call": round(td / calls * 1e6, 2),
-            "calls": calls, "note": "poporon_encode / poporon_decode (16 errors), one codeword per call, host "
-                                    "buffers, called through ctypes (~1 us of that per call)"}
+            "python_ctypes_encode_us_per_call": round(tpe / calls * 1e6, 2),
+            "python_ctypes_decode16_us_per_call": round(tpd / calls * 1e6, 2),
+            "calls": calls, "note": "poporon_encode / poporon_decode (16 errors), one codeword per call, host buffers, "
+                                    "a C loop (as cpu_baseline's T1 loop of the reference); python_ctypes_*: the same "
+                                    "calls from a Python loop"}
 
 
 def _cpu_info():
@@ -1053,19 +1081,26 @@ def main(argv=None):
         if "decode_mixed" in line:
             line["decode_mixed"].pop("_kt", None)
             line["decode_mixed"].pop("_steps", None)
+    del w
+    if not args.no_c4:
+        c4 = run_strong(be, ranks, args, rank, world)
+        samples.update(c4.pop("_samples"))
+        line["configs4"] = c4
+        line["parity_checksum"] = c4["parity_checksum"]
+        line["verified"] = line["verified"] and c4["verified"]
     # every sampled codeword of every mode against the reference CPU path
     # (after all timed loops)
     ps = parity_sample(samples, ranks)
     line["parity_sample"] = ps
     line["verified"] = line["verified"] and all(v["mismatches"] == 0 for k, v in ps.items() if isinstance(v, dict))
-    del w
-    if not args.no_c4:
-        c4 = run_strong(be, ranks, args, rank, world)
-        line["configs4"] = c4
-        line["parity_checksum"] = c4["parity_checksum"]
-        line["verified"] = line["verified"] and c4["verified"]
     if gpu and rank == 0 and world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline()
+        lat = line.get("single_call_latency")
+        if lat:  # the drop-in path against the reference on one host core, same box and run
+            t1 = line["cpu_baseline"]["T1"]
+            lat["vs_reference_T1"] = {"encode": round(t1["encode_us_per_cw"] / lat["encode_us_per_call"], 3),
+                                      "decode16": round(t1["decode16_us_per_cw"] / lat["decode16_us_per_call"], 3),
+                                      "note": "> 1: the GPU call is faster than the reference's call on one core"}
     if rank == 0:
         print(json.dumps(line), flush=True)
     if world > 1:

@@ -744,8 +744,10 @@ static void gpu_release(GpuCtx &g)
     if (g.hstage)
         (void)hipHostFree(g.hstage);
     if (g.sstream) {
-        if (g.zc) /* ask a live server to leave now rather than at its idle limit */
-            *reinterpret_cast<volatile uint32_t *>(g.zc + ZC_STOP) = 1u;
+        if (g.zc && g.srv_on) { /* ask a live server to leave now rather than at its idle limit */
+            volatile uint32_t *req = reinterpret_cast<volatile uint32_t *>(g.zc + ZC_REQ);
+            *req = ZC_REQ_WORD(g.zc_seq + 1u, RS_SRV_STOP, 0u, 0u);
+        }
         (void)hipStreamSynchronize(g.sstream);
         (void)hipStreamDestroy(g.sstream);
     }
@@ -1902,7 +1904,6 @@ static bool srv_launch(poporon_t *h, uint32_t last)
     GpuCtx &g = h->gpu;
     if (!g.sstream)
         HIP_OK(hipStreamCreateWithFlags(&g.sstream, hipStreamNonBlocking));
-    *reinterpret_cast<volatile uint32_t *>(g.zc + ZC_STOP) = 0u;
     const uint32_t id = g.srv_id + 1u;
     RsCorrParams prm = h->corr;
     HIP_OK(rsk_serve(g.tab, &prm, g.zc_dev, last, id, SRV_IDLE_TICKS, SRV_MAX_TICKS, g.sstream));

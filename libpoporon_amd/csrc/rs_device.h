@@ -206,10 +206,10 @@ hipError_t rsk_serve(const RsDevTables *tab, const RsCorrParams *prm, uint8_t *z
 #define ZC_REQ_MODE(w) (((w) >> 10) & 3u) /* decode mode (rsk_decode1) */
 #define ZC_REQ_SIZE(w) ((w) & 0xFFu)      /* message bytes (1..223) */
 #define ZC_EXITED 768 /* u32: the id of the last server launch that has left */
-#define ZC_STOP 832  /* u32: nonzero asks the server to leave */
 #define ZC_BYTES 1024
 #define RS_SRV_ENCODE 1u
 #define RS_SRV_DECODE 2u
+#define RS_SRV_STOP 3u   /* the server leaves (poporon_destroy) */
 
 /* poly syndromes (32 B per codeword, rsk_syndrome) -> log form: out[c*stride + i]
  * = log S_i (255 = zero), flag[c] = any S_i nonzero; out / flag may be NULL */

@@ -156,12 +156,6 @@ __global__ __launch_bounds__(BWG, BM_WAVES) void rs_bm_k(const RsDevTables *__re
         auto step = [&](auto sc, uint32_t r) __attribute__((always_inline)) {
             constexpr int s = decltype(sc)::value;
             const uint32_t ub = ubp;
-            /* the updated Lambda's degree bound and its wave maximum depend
-             * only on the previous iteration's bounds, not on this
-             * discrepancy: formed first, the DPP chain overlaps the
-             * discrepancy's lookups instead of following them */
-            const uint32_t up = min((uint32_t)(NL - 1), max(dl, db + 1u));
-            const uint32_t ub2 = wave_max_full(up);
             uint32_t la[NL];
             uint32_t disc = 0;
             la[0] = pofs;
@@ -188,6 +182,10 @@ __global__ __launch_bounds__(BWG, BM_WAVES) void rs_bm_k(const RsDevTables *__re
             const uint32_t b16 = B[NL - 1] != AZ;
             over |= upd ? (bo | b16) : 0u;
             bo = lengthen ? 0u : (bo | b16);
+            /* (formed before the discrepancy instead, to overlap its lookups:
+             * unchanged, profiles/r04_bm_hoist_ab.log) */
+            const uint32_t up = min((uint32_t)(NL - 1), max(dl, db + 1u));
+            const uint32_t ub2 = wave_max_full(up);
             ubp = ub2;
             const uint64_t lmask = __ballot(lengthen);
             static_for<0, (NL - 1) / 4 + 1, 1>([&](auto mc) __attribute__((always_inline)) {

@@ -606,7 +606,7 @@ extern "C" hipError_t rsk_decode1(const RsDevTables *tab, const RsCorrParams *pr
  * The tables are filled once per launch.
  *
  * Every launch ends on its own: after idle_ticks of s_memrealtime (100 MHz)
- * without a request, after max_ticks in all, or when the host sets ZC_STOP
+ * without a request, after max_ticks in all, or at an RS_SRV_STOP request
  * (poporon_destroy).  It then stores its launch id to ZC_EXITED and serves
  * nothing more; a request the host posted meanwhile is seen unserved there
  * and the host launches a new server for it (api.cpp srv_call), on the same
@@ -625,20 +625,18 @@ __global__ __launch_bounds__(S1_WG) void rs_serve_k(const RsDevTables *__restric
     uint64_t idle0 = t0;
     for (;;) {
         if (t == 0) {
+            /* the whole request is one word: one PCIe round trip per poll */
             uint32_t r = last, op = 0;
             for (;;) {
-                /* one PCIe round trip per poll: the whole request is this word */
                 r = __hip_atomic_load(req, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
                 if (r != last) {
-                    op = ZC_REQ_OP(r);
+                    op = ZC_REQ_OP(r); /* RS_SRV_STOP: leave */
                     cmd[2] = ZC_REQ_SIZE(r);
                     cmd[3] = ZC_REQ_MODE(r);
                     break;
                 }
-                const uint32_t stop = __hip_atomic_load(reinterpret_cast<uint32_t *>(zc + ZC_STOP), __ATOMIC_RELAXED,
-                                                        __HIP_MEMORY_SCOPE_SYSTEM);
                 const uint64_t now = __builtin_amdgcn_s_memrealtime();
-                if (stop || now - idle0 > idle_ticks || now - t0 > max_ticks)
+                if (now - idle0 > idle_ticks || now - t0 > max_ticks)
                     break; /* op = 0: leave */
                 __builtin_amdgcn_s_sleep(1);
             }
@@ -647,8 +645,9 @@ __global__ __launch_bounds__(S1_WG) void rs_serve_k(const RsDevTables *__restric
         }
         __syncthreads();
         const uint32_t seq = cmd[0], op = cmd[1], size = cmd[2], mode = cmd[3];
-        if (op == 0u || size == 0u || size > 223u)
-            break; /* uniform (a malformed request also ends the launch: the host sees it unserved) */
+        if ((op != RS_SRV_ENCODE && op != RS_SRV_DECODE) || size == 0u || size > 223u)
+            break; /* uniform: idle, lifetime, RS_SRV_STOP; a malformed request also ends the
+                    * launch (the host sees it unserved) */
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, ""); /* this wave's loads of the payload: after the request */
         if (op == RS_SRV_ENCODE) {
             enc1_body(s.g, reinterpret_cast<uint32_t(*)[8]>(s.part), T, zc + ZC_DATA, zc + ZC_PAR, size);

@@ -44,6 +44,9 @@ def load():
             fn = getattr(lib, name)
             fn.restype = C.c_bool
             fn.argtypes = args
+        lib.ptu_time_encode.restype = lib.ptu_time_decode.restype = C.c_double
+        lib.ptu_time_encode.argtypes = [vp, vp, vp, u64, vp, u64, u64]
+        lib.ptu_time_decode.argtypes = [vp, vp, vp, u64, vp, u64, u64, u64, vp, vp]
         _lib = lib
     return _lib
 
@@ -65,6 +68,29 @@ def synth_errors(seed, first, count, nerr, span, d_pos, d_mag, sorted_positions=
 
 def channel_xor(d_pos, d_mag, per_row, d_rows, stride, count, stream=0):
     _ok(load().ptu_channel_xor(d_pos, d_mag, per_row, d_rows, stride, count, stream or None), "ptu_channel_xor")
+
+
+def _vp(a):
+    return a.ctypes.data_as(C.c_void_p)
+
+
+def time_encode(lib, h, msgs, par):
+    """A C loop of lib.poporon_encode (lib: a ctypes CDLL) on handle h:
+    msgs[c] (size bytes) -> par[c]; returns seconds (< 0: a call failed)."""
+    n, size = msgs.shape
+    return load().ptu_time_encode(C.cast(lib.poporon_encode, C.c_void_p), h, _vp(msgs), size, _vp(par), par.shape[1],
+                                  n)
+
+
+def time_decode(lib, h, data, par):
+    """A C loop of lib.poporon_decode on handle h over the rows data[c] /
+    par[c], decoded in place; returns (seconds, ok u8[n], corrected u8[n])."""
+    n, size = data.shape
+    ok = np.zeros(n, np.uint8)
+    cor = np.zeros(n, np.uint8)
+    t = load().ptu_time_decode(C.cast(lib.poporon_decode, C.c_void_p), h, _vp(data), size, _vp(par), par.shape[1],
+                               size, n, _vp(ok), _vp(cor))
+    return t, ok, cor
 
 
 def checksum(d_rows, stride, width, first, count, d_sum, stream=0):

@@ -7,6 +7,12 @@
  *   ptu_synth_errors    per-row unique error positions + nonzero magnitudes
  *   ptu_channel_xor     symbol-error channel (XOR magnitudes into positions)
  *   ptu_checksum        order-independent 64-bit checksum of a row batch
+ *   ptu_time_encode / ptu_time_decode
+ *                       a C loop of single-codeword calls through function
+ *                       pointers (poporon_encode / poporon_decode of
+ *                       whichever library the caller resolved): the
+ *                       reference's calling pattern timed without any
+ *                       interpreter overhead, as the CPU baseline's C loop is
  *
  * Every value depends only on (seed, global row index), so any sharding of a
  * batch over ranks produces the same rows; testutil/__init__.py restates each
@@ -15,6 +21,8 @@
 #include <hip/hip_runtime.h>
 #include <stddef.h>
 #include <stdint.h>
+
+#include <chrono>
 
 #define PTU_EXPORT extern "C" __attribute__((visibility("default")))
 
@@ -193,4 +201,38 @@ PTU_EXPORT bool ptu_checksum(const uint8_t *d_rows, uint64_t stride, uint32_t wi
     hipLaunchKernelGGL(checksum_k, dim3(g), dim3(256), 0, (hipStream_t)stream, d_rows, stride, width, first, count,
                        (unsigned long long *)d_sum);
     return hipGetLastError() == hipSuccess;
+}
+
+/* ------------------------------------------------------------------------ */
+/* single-call latency loops (host code)                                    */
+/* ------------------------------------------------------------------------ */
+typedef bool (*ptu_enc_fn)(void *, uint8_t *, size_t, uint8_t *);
+typedef bool (*ptu_dec_fn)(void *, uint8_t *, size_t, uint8_t *, size_t *);
+
+/* calls x enc(h, msgs + c * size, size, par + c * pstride); seconds, or -1
+ * if a call failed */
+PTU_EXPORT double ptu_time_encode(void *fn, void *h, uint8_t *msgs, uint64_t size, uint8_t *par, uint64_t pstride,
+                                  uint64_t calls)
+{
+    const ptu_enc_fn enc = (ptu_enc_fn)fn;
+    const auto t0 = std::chrono::steady_clock::now();
+    for (uint64_t c = 0; c < calls; ++c)
+        if (!enc(h, msgs + c * size, size, par + c * pstride))
+            return -1.0;
+    return std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+}
+
+/* calls x dec(h, data + c * dstride, size, par + c * pstride, &n), ok / corrected
+ * recorded per call; seconds */
+PTU_EXPORT double ptu_time_decode(void *fn, void *h, uint8_t *data, uint64_t dstride, uint8_t *par, uint64_t pstride,
+                                  uint64_t size, uint64_t calls, uint8_t *ok, uint8_t *cor)
+{
+    const ptu_dec_fn dec = (ptu_dec_fn)fn;
+    const auto t0 = std::chrono::steady_clock::now();
+    for (uint64_t c = 0; c < calls; ++c) {
+        size_t n = 0;
+        ok[c] = dec(h, data + c * dstride, size, par + c * pstride, &n) ? 1 : 0;
+        cor[c] = (uint8_t)n;
+    }
+    return std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
 }
