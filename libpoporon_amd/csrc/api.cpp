@@ -1178,9 +1178,10 @@ static bool launch_split(poporon_t *h, const RsCorrParams &prm, const RsSplitWs 
         t.done();
     }
     {
+        /* what the split kernels hand on: one wave per codeword (rs_list1_k) */
         KernelTimer t(g, POPORON_AMD_KERNEL_LIST, s);
-        HIP_OK(rsk_correct_list(g.tab, &prm, d_data, ds, d_par, ps, count, ws.syn, ws.list, ws.nlist, ok,
-                                corrected, g.num_cu, s));
+        HIP_OK(rsk_list1(g.tab, &prm, d_data, ds, d_par, ps, count, ws.syn, ws.list, ws.nlist, ok, corrected,
+                         g.num_cu, s));
         t.done();
     }
     return true;

@@ -211,6 +211,13 @@ hipError_t rsk_serve(const RsDevTables *tab, const RsCorrParams *prm, uint8_t *z
 #define RS_SRV_DECODE 2u
 #define RS_SRV_STOP 3u   /* the server leaves (poporon_destroy) */
 
+/* the split error-mode decode's list, one wave per codeword (rs_single.hip
+ * rs_list1_k): the codewords list[0 .. *list_n) decoded from their poly
+ * syndromes and corrected in place; count bounds the grid */
+hipError_t rsk_list1(const RsDevTables *tab, const RsCorrParams *prm, uint8_t *data, size_t dstride, uint8_t *parity,
+                     size_t pstride, size_t count, const uint8_t *syn, const uint32_t *list, const uint32_t *list_n,
+                     uint8_t *ok, uint8_t *corrected, int num_cu, hipStream_t stream);
+
 /* poly syndromes (32 B per codeword, rsk_syndrome) -> log form: out[c*stride + i]
  * = log S_i (255 = zero), flag[c] = any S_i nonzero; out / flag may be NULL */
 hipError_t rsk_syn_log(const RsDevTables *tab, const uint8_t *syn, size_t count, uint16_t *out, size_t stride,

@@ -677,3 +677,235 @@ extern "C" hipError_t rsk_serve(const RsDevTables *tab, const RsCorrParams *prm,
                        max_ticks);
     return hipGetLastError();
 }
+
+/* ------------------------------------------------------------------------ */
+/* the split decode's list: one wave per codeword                            */
+/* ------------------------------------------------------------------------ */
+
+/*
+ * rs_list1_k: the error-mode codewords the split kernels hand on (L > 16, a
+ * locator past x^16, deg != L: beyond capacity, the reference's failures and
+ * miscorrections), decoded one codeword per WAVE with dec1_body's steps
+ * (src/decode.c:49-227 with its integer semantics): Berlekamp-Massey with
+ * coefficient i on lane i, Chien with four points per lane, Omega, Forney and
+ * the re-syndrome check split over the two 32-lane halves, the corrections
+ * applied in place.  A list is a few percent of a batch (~7 % of the
+ * codewords of a binomial channel with mean 11.5 errors): one codeword per
+ * lane put a few waves on each SIMD, each a ~10^4-step serial chain (0.24 ms
+ * for 74k codewords of 2^20); one per wave puts the work of a codeword on 64
+ * lanes and 32 waves on every CU.
+ *
+ * Four waves per workgroup share the GF tables; each wave loops over list
+ * entries on its own (no workgroup barrier after the table fill).
+ */
+#define L1_WG 256
+
+struct List1Wave {
+    uint32_t slog[64];  /* log S_i (ZL: zero), i < 32; ZL at 32..63 */
+    uint32_t spoly[32];
+    uint32_t llam[64];  /* log Lambda_j (ZL: zero), j <= 32; ZL past */
+    uint32_t lom[32];
+    uint32_t roots[32], locs[32], mags[32];
+};
+
+struct List1Smem {
+    Tabs g;
+    List1Wave w[L1_WG / 64];
+};
+
+/* lane order within a wave: LDS writes by some lanes, then reads by others */
+__device__ __forceinline__ void wave_sync()
+{
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+/* v of lane l ^ 32 (the other half of the wave): the swap's first result
+ * holds, in every lane, the low half's value, the second the high half's */
+__device__ __forceinline__ uint32_t other_half(uint32_t v, uint32_t lane)
+{
+    const auto a = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+    return lane < 32u ? a[1] : a[0];
+}
+
+__global__ __launch_bounds__(L1_WG) void rs_list1_k(const RsDevTables *__restrict__ T, RsCorrParams P, uint8_t *data,
+                                                    size_t dstride, uint8_t *parity, size_t pstride,
+                                                    const uint8_t *__restrict__ syn, const uint32_t *__restrict__ list,
+                                                    const uint32_t *__restrict__ list_n, uint8_t *__restrict__ okp,
+                                                    uint8_t *__restrict__ corp)
+{
+    const uint32_t n = *list_n;
+    if ((size_t)blockIdx.x * (L1_WG / 64) >= n)
+        return;
+    __shared__ List1Smem sm;
+    const uint32_t t = threadIdx.x, lane = t & 63u, wave = t >> 6;
+    fill_tabs(sm.g, T, t);
+    __syncthreads();
+    const Tabs &g = sm.g;
+    List1Wave &s = sm.w[wave];
+    const uint32_t size = P.size, L = size + RS_NR;
+    const int32_t pad = P.pad;
+    const bool co = lane <= RS_NR;
+    for (uint32_t e = blockIdx.x * (L1_WG / 64) + wave; e < n; e += gridDim.x * (L1_WG / 64)) {
+        const size_t cw = list[e];
+        /* ---- syndromes (poly form, rsk_syndrome) -> log form ---- */
+        const uint32_t v = lane < RS_NR ? syn[cw * RS_NR + lane] : 0u;
+        if (lane < RS_NR)
+            s.spoly[lane] = v;
+        s.slog[lane] = lane < RS_NR ? (uint32_t)g.lg[v] : ZL;
+        wave_sync();
+
+        /* ---- Berlekamp-Massey, error mode (r = 1..32): dec1_body's loop
+         * with no erasures ---- */
+        uint32_t lam = lane == 0 ? 1u : 0u;
+        uint32_t llam = g.lg[lam];
+        uint32_t B = llam, Lr = 0;
+        uint32_t term = g.ex[llam + s.slog[lane == 0 ? 0u : 63u]];
+        uint32_t s1 = s.slog[lane <= 1u ? 1u - lane : 63u];
+        for (uint32_t r = 1u; r <= RS_NR; ++r) {
+            const uint32_t disc = wave_xor_v(term);
+            const uint32_t bs = wave_up_old(B, ZL);
+            const uint32_t ld = g.lg[disc];
+            const uint32_t dq = red(ld + bs);
+            const uint32_t t1 = g.ex[llam + s1], t2 = g.ex[dq + s1], up = g.ex[dq];
+            s1 = s.slog[lane <= r + 1u && r + 1u < RS_NR ? r + 1u - lane : 63u];
+            term = t1 ^ t2;
+            const uint32_t ds = __builtin_amdgcn_readfirstlane(disc);
+            const bool len = ds != 0u && 2u * Lr <= r - 1u; /* uniform */
+            const uint32_t bl = lam ? red(llam + 255u - ld) : ZL;
+            B = len ? bl : bs;
+            Lr = len ? r - Lr : Lr;
+            lam ^= up;
+            llam = g.lg[lam];
+        }
+        const uint64_t nz = __ballot(co && lam != 0u);
+        const uint32_t deg = 63u - (uint32_t)__builtin_clzll(nz); /* lane 0 holds Lambda_0 = 1 */
+        s.llam[lane] = co ? llam : ZL;
+        wave_sync();
+        uint32_t ok = 0, fixed = 0;
+        bool fail = deg == 0u; /* src/decode.c:108-110 */
+
+        /* ---- Chien, src/decode.c:117-145: points i = 64 k + lane + 1 ---- */
+        uint32_t total = 0;
+        if (!fail) {
+#pragma unroll 1
+            for (uint32_t k = 0; k < 4; ++k) {
+                const uint32_t i = 64u * k + lane + 1u, ii = i == 255u ? 0u : i;
+                uint32_t ev = 1u, ex = 0;
+#pragma unroll 8
+                for (uint32_t j = 1; j <= deg; ++j) {
+                    ex = red(ex + ii);
+                    ev ^= g.ex[s.llam[j] + ex];
+                }
+                const bool root = i <= 255u && ev == 0u;
+                const uint64_t rb = __ballot(root);
+                if (root) {
+                    const uint32_t idx = total + (uint32_t)__builtin_popcountll(rb & ((1ull << lane) - 1ull));
+                    const uint32_t loc = (i * P.iprim + 254u) % 255u;
+                    if (idx < RS_NR) {
+                        s.roots[idx] = i;
+                        s.locs[idx] = loc;
+                    }
+                }
+                fail |= __ballot(root && (int32_t)((i * P.iprim + 254u) % 255u) < pad) != 0ull; /* :132-134 */
+                total += (uint32_t)__builtin_popcountll(rb);
+            }
+            fail |= total != deg; /* src/decode.c:143-145 */
+        }
+        wave_sync();
+
+        if (!fail) {
+            /* ---- Omega_m = sum_(j <= m) S_(m-j) Lambda_j, m < deg: lane m
+             * and lane m + 32 each take half of the terms ---- */
+            const uint32_t m = lane & 31u, j0 = (lane >> 5) * 16u;
+            uint32_t acc = 0;
+#pragma unroll
+            for (uint32_t j = j0; j < j0 + 16u; ++j) /* j > m reads slog[32..63] = ZL */
+                acc ^= g.ex[s.slog[(m - j) & 63u] + s.llam[j]];
+            acc ^= other_half(acc, lane);
+            if (lane < RS_NR)
+                s.lom[lane] = lane < deg ? (uint32_t)g.lg[acc] : ZL;
+            wave_sync();
+
+            /* ---- Forney, src/decode.c:159-191: root q = lane & 31; the low
+             * half sums the numerator, the high half the denominator ---- */
+            const uint32_t q = lane & 31u;
+            const uint32_t rt = q < deg ? s.roots[q] : 0u, rm = rt % 255u;
+            uint32_t part = 0;
+            if (lane < 32u) {
+#pragma unroll 8
+                for (uint32_t mm = 0; mm < RS_NR; ++mm) /* Omega is ZL past deg - 1 */
+                    part ^= g.ex[s.lom[mm] + (mm * rm) % 255u];
+            } else {
+#pragma unroll 8
+                for (uint32_t h = 0; h <= 30u; h += 2u) /* Lambda is ZL past the degree */
+                    part ^= g.ex[s.llam[h + 1u] + (h * rm) % 255u];
+            }
+            const uint32_t oth = other_half(part, lane);
+            const uint32_t num = lane < 32u ? part : oth, den = lane < 32u ? oth : part;
+            uint32_t mag = 0;
+            if (q < deg && num) {
+                const uint32_t l2 = ((uint32_t)((int32_t)rt * ((int32_t)P.fcr - 1) + (int32_t)RS_NN) & 0xffffu) % 255u;
+                const uint32_t lden = den ? (uint32_t)g.lg[den] : 255u; /* no den = 0 guard */
+                mag = g.ex[(g.lg[num] + l2 + RS_NN - lden) % 255u];
+            }
+            fixed = (uint32_t)__builtin_popcountll(__ballot(lane < 32u && q < deg && num != 0u)); /* Q6 */
+            if (lane < 32u) {
+                s.mags[q] = mag;
+                if (q >= deg)
+                    s.locs[q] = 0;
+            }
+            wave_sync();
+
+            /* ---- re-syndrome check, src/decode.c:193-209 (int16 exponent,
+             * uint16 gf_mod): syndrome i = lane & 31, roots split over the
+             * halves ---- */
+            const uint32_t i = lane & 31u, q0 = (lane >> 5) * 16u;
+            const int32_t ci = (int32_t)(P.fcr + i) * (int32_t)P.prim;
+            uint32_t chk = 0;
+#pragma unroll 4
+            for (uint32_t qq = q0; qq < q0 + 16u; ++qq) {
+                const uint32_t mg = s.mags[qq];
+                const int16_t k16 = (int16_t)(ci * (int32_t)(RS_NN - 1u - s.locs[qq]));
+                const uint32_t x = ((uint32_t)((int32_t)g.lg[mg] + (int32_t)k16) & 0xffffu) % 255u;
+                chk ^= mg ? (uint32_t)g.ex[x] : 0u;
+            }
+            chk ^= other_half(chk, lane);
+            fail |= __ballot(lane < 32u && chk != s.spoly[i]) != 0ull;
+
+            /* ---- apply, src/decode.c:215-226 (error mode): locations from
+             * Chien lie in [pad, 254], so none is out of range ---- */
+            if (!fail) {
+                ok = 1;
+                if (lane < deg) {
+                    const uint32_t p = (uint32_t)((int32_t)s.locs[lane] - pad);
+                    if (mag && p < L) {
+                        uint8_t *d = p < size ? data + cw * dstride + p : parity + cw * pstride + (p - size);
+                        *d = (uint8_t)(*d ^ mag);
+                    }
+                }
+            }
+        }
+        if (lane == 0) {
+            okp[cw] = (uint8_t)ok;
+            if (corp)
+                corp[cw] = (uint8_t)fixed;
+        }
+        wave_sync(); /* this codeword's LDS reads before the next one's writes */
+    }
+}
+
+extern "C" hipError_t rsk_list1(const RsDevTables *tab, const RsCorrParams *prm, uint8_t *data, size_t dstride,
+                                uint8_t *parity, size_t pstride, size_t count, const uint8_t *syn, const uint32_t *list,
+                                const uint32_t *list_n, uint8_t *ok, uint8_t *corrected, int num_cu, hipStream_t stream)
+{
+    if (count == 0)
+        return hipSuccess;
+    /* eight 4-wave workgroups per CU (32 waves), fewer for a small batch;
+     * workgroups past the list's length (read on the device) leave at once */
+    const size_t cap = 8u * (size_t)(num_cu > 0 ? num_cu : 256), need = (count + 3) / 4;
+    RS_LAUNCH(rs_list1_k, dim3((uint32_t)(need < cap ? need : cap)), dim3(L1_WG), 0, stream, tab, *prm, data, dstride,
+              parity, pstride, syn, list, list_n, ok, corrected);
+    return hipGetLastError();
+}
