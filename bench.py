@@ -521,10 +521,10 @@ def run_erasure(be, ranks, args, rank, world, w, ne=32, nerr=0):
     eclean = be.like(cw)
     be.copy(eclean, cw)
     es = max(3, args.steps // 2)
-    ecopies = (es + 1) * B * N <= 0.5 * be.free_bytes()
+    ecopies = (2 * es + 1) * B * N <= 0.5 * be.free_bytes()
     ebad = []
     if ecopies:
-        for _ in range(es + 1):
+        for _ in range(2 * es + 1):
             b = be.like(cw)
             be.copy(b, eclean)
             be.channel(b, (pos, emag))
@@ -539,13 +539,18 @@ def run_erasure(be, ranks, args, rank, world, w, ne=32, nerr=0):
         be.decode(d, w["st"], erasures=(slots, cnts))
 
     estep(0)
+    # timed loop (cw_per_s): no per-kernel events; then the same decodes on
+    # fresh copies with the events on (kernel times), as in run_weak
     ranks.barrier(be.sync)
-    be.rs.timing(True)
     t0 = time.perf_counter()
     for k in range(es):
         estep(1 + k)
     ranks.barrier(be.sync)
     et = ranks.max(time.perf_counter() - t0)
+    be.rs.timing(True)
+    for k in range(es):
+        estep(1 + es + k if ecopies else 0)
+    be.sync()
     ekt = {k: be.rs.timing_read(k) for k in be.P.KERNEL_NAMES}
     ekt = {k: v for k, v in ekt.items() if v[1]}
     kms = sum(ms / es for ms, n in ekt.values())
@@ -556,7 +561,7 @@ def run_erasure(be, ranks, args, rank, world, w, ne=32, nerr=0):
     enbad = ranks.sum_int(enbad)
     idx = sample_index(B)
     sample = {"in": channel_rows(be.host(eclean, idx), be.host(pos, idx), be.host(emag, idx)),
-              "out": be.host(ebad[es] if ecopies else cw, idx), "ok": be.host(w["st"][0], idx),
+              "out": be.host(ebad[2 * es] if ecopies else cw, idx), "ok": be.host(w["st"][0], idx),
               "cor": be.host(w["st"][1], idx), "slots": be.host(slots, idx), "cnt": be.host(cnts, idx),
               "first": first}
     return {"cw_per_s": round(B * world * es / et, 1),
@@ -599,9 +604,9 @@ def run_mixed(be, ranks, args, rank, world, w):
     be.mask_errors(mag, ne)
     cw = w["clean"]
     es = max(3, args.steps // 2)
-    mcopies = (es + 1) * B * N <= 0.5 * be.free_bytes()
+    mcopies = (2 * es + 1) * B * N <= 0.5 * be.free_bytes()
     mbad = []
-    for _ in range(es + 1 if mcopies else 1):
+    for _ in range(2 * es + 1 if mcopies else 1):
         b = be.like(cw)
         be.copy(b, cw)
         be.channel(b, (pos, mag))
@@ -620,19 +625,21 @@ def run_mixed(be, ranks, args, rank, world, w):
     mstep(0)
     ranks.barrier(be.sync)
     gpu = be.kind == "gpu"
-    if gpu:
-        be.rs.timing(True)
     t0 = time.perf_counter()
     for k in range(es):
         mstep(1 + k if mcopies else 0)
     ranks.barrier(be.sync)
     et = ranks.max(time.perf_counter() - t0)
     mkt = {}
-    if gpu:
+    if gpu:  # kernel times from a second loop with the per-kernel events on
+        be.rs.timing(True)
+        for k in range(es):
+            mstep(1 + es + k if mcopies else 0)
+        be.sync()
         mkt = {k: be.rs.timing_read(k) for k in be.P.KERNEL_NAMES}
         mkt = {k: v for k, v in mkt.items() if v[1]}
         be.rs.timing(False)
-    last = mbad[es] if mcopies else mbad[0]
+    last = mbad[(2 * es if gpu else es)] if mcopies else mbad[0]
     nbad = ranks.sum_int(be.n_bad_mixed(st, ne, last, cw))
     idx = sample_index(B)
     sample = {"in": channel_rows(be.host(cw, idx), be.host(pos, idx), be.host(mag, idx)), "out": be.host(last, idx),
