@@ -882,6 +882,180 @@ __global__ __launch_bounds__(EWG, ERA_WAVES) void rs_era_k(const RsDevTables *__
     }
 }
 
+/*
+ * rs_era_bp_k: the same codewords and output as rs_era_k, with the magnitudes
+ * solved directly.  With 32 erasures the 32 syndromes determine them: S_i =
+ * sum_l z_l X_l^i (i < 32, z_l = Y_l X_l^fcr) is a square Vandermonde system
+ * with distinct nodes, whatever the syndromes are, and the reference's
+ * Forney step (src/decode.c:159-191) computes its unique solution (its
+ * re-syndrome check passes by construction; for the parameters that reach
+ * this kernel -- RsCorrParams.vfast, prim 1 -- its uint16 exponent of
+ * alpha^(root (fcr-1)) does not wrap).  So any exact solver gives the
+ * reference's bytes: here the Bjorck-Pereyra algorithm for the primal
+ * Vandermonde system (Golub & Van Loan, Alg. 4.6.2), in GF(2^8):
+ *
+ *   for k = 0..30:     for i = 31 down to k+1:  b_i ^= X_k b_(i-1)
+ *   for k = 30 .. 0:   for i = k+1 .. 31:       b_i /= X_i ^ X_(i-k-1)
+ *                      for i = k .. 30:         b_i ^= b_(i+1)
+ *
+ * then Y_l = z_l X_l^-fcr = alpha^(log z_l + fcr (slot_l + pad + 1)).  Per
+ * codeword 496 multiply-adds (2 lookups, 3 VALU) and 496 divisions (3
+ * lookups, 6 VALU) + 496 XORs, against the locator (831 lookups), Omega (528)
+ * and Forney (1,536) of the Forney route.  The b_i and X_l live as
+ * "log-entry addresses" hz | v << 7 (GfA::hz): a log is one ds_read_u16 at
+ * that address, an XOR of two values is one v_bitop3 ((A ^ B) | hz), and a
+ * division b / D is alpha^(log b - log D) read at loga(b) - loga(D) + pofs +
+ * 255 * 128 (a zero b lands on a byte 0 of the table, no test).
+ * (Prototype against the oracle over fcr 0, 1, 2, 5, 97, sizes 223 and 100,
+ * extra errors besides the erasures: bit-exact.)
+ */
+__global__ __launch_bounds__(EWG, ERA_WAVES) void rs_era_bp_k(const RsDevTables *__restrict__ T, RsCorrParams P,
+                                                            const uint8_t *__restrict__ syn,
+                                                            const uint8_t *__restrict__ pos8, size_t pos_stride,
+                                                            const uint8_t *__restrict__ cntp, size_t count,
+                                                            uint8_t *__restrict__ rec, uint8_t *__restrict__ meta,
+                                                            uint32_t *__restrict__ list, uint32_t *__restrict__ nlist,
+                                                            uint8_t *__restrict__ ok, uint8_t *__restrict__ corrected,
+                                                            uint32_t pend)
+{
+    __shared__ uint32_t lgf[512 * 32];
+    fill_gfa<EWG>(lgf, T);
+    __syncthreads();
+    const GfA gf{lds_addr(lgf) + 4u * (threadIdx.x & 31u) + 1u};
+    const uint32_t pofs = gf.pofs, hz = gf.hz();
+    const uint32_t lim = P.size + RS_NR, pad = (uint32_t)P.pad;
+
+    uint32_t it = 0;
+    for (size_t base = (size_t)blockIdx.x * EWG; base < count; base += (size_t)gridDim.x * EWG, ++it) {
+        prio_by_progress(it);
+        const size_t cw = base + threadIdx.x;
+        const bool valid = cw < count;
+        uint4 sa = make_uint4(0, 0, 0, 0), sb = sa, pa = sa, pb = sa;
+        uint32_t ne = 0;
+        const uint8_t *slots = pos8 + (valid ? cw : 0) * pos_stride;
+        if (valid) {
+            sa = reinterpret_cast<const uint4 *>(syn)[2 * cw];
+            sb = reinterpret_cast<const uint4 *>(syn)[2 * cw + 1];
+            pa = reinterpret_cast<const uint4 *>(slots)[0];
+            pb = reinterpret_cast<const uint4 *>(slots)[1];
+            ne = cntp[cw];
+        }
+        const bool any = (sa.x | sa.y | sa.z | sa.w | sb.x | sb.y | sb.z | sb.w) != 0u;
+        uint32_t pk[RS_NR / 4] = {pa.x, pa.y, pa.z, pa.w, pb.x, pb.y, pb.z, pb.w};
+        bool asc = true;
+        uint32_t prev = pk[0] & 0xffu;
+#pragma unroll
+        for (int n = 1; n < RS_NR; ++n) {
+            const uint32_t p = (pk[n >> 2] >> (8 * (n & 3))) & 0xffu;
+            asc = asc && p > prev;
+            prev = p;
+        }
+        const bool fast = valid && any && ne == RS_NR && asc && prev < lim;
+        if (valid && !fast) {
+            if (!any) {
+                ok[cw] = 1;
+                if (corrected)
+                    corrected[cw] = 0;
+                meta[cw] = (uint8_t)(RS_ST_DONE << 5);
+            } else if (pend) { /* the errata kernels (rs_errata.hip) decode it */
+                meta[cw] = (uint8_t)(RS_ST_PEND << 5);
+            } else {
+                meta[cw] = (uint8_t)(RS_ST_LIST << 5);
+                list[atomicAdd(nlist, 1u)] = (uint32_t)cw;
+            }
+        }
+        const uint64_t pw = __ballot(valid && any && !fast && pend);
+        if (pw != 0ull && (threadIdx.x & 63u) == (uint32_t)__builtin_ctzll(pw))
+            nlist[1] = 1u; /* the errata kernels run only if some codeword is pending: one store per wave */
+        if (__ballot(fast) == 0ull) /* uniform */
+            continue;
+        uint32_t *recw = reinterpret_cast<uint32_t *>(rec + (valid ? cw : 0) * 64u);
+        if (fast) { /* the record's slots */
+            reinterpret_cast<uint4 *>(recw)[0] = pa;
+            reinterpret_cast<uint4 *>(recw)[1] = pb;
+        }
+        if (!fast) { /* lanes along for the ride: distinct in-range nodes (no division by zero matters) */
+#pragma unroll
+            for (int k = 0; k < RS_NR / 4; ++k)
+                pk[k] = 0x03020100u + 0x04040404u * (uint32_t)k;
+        }
+        auto slot = [&](int l) __attribute__((always_inline)) { return (pk[l >> 2] >> (8 * (l & 3))) & 0xffu; };
+
+        /* b_i = S_i and X_l as log-entry addresses */
+        uint32_t hb[RS_NR], hx[RS_NR];
+        {
+            const uint32_t sw[8] = {sa.x, sa.y, sa.z, sa.w, sb.x, sb.y, sb.z, sb.w};
+#pragma unroll
+            for (int i = 0; i < RS_NR; ++i)
+                hb[i] = hz | (((sw[i >> 2] >> (8 * (i & 3))) & 0xffu) << 7);
+        }
+#pragma unroll
+        for (int l = 0; l < RS_NR; ++l)
+            hx[l] = hz | shl7(gf.exp(RS_NN - 1u - (slot(l) + pad))); /* X_l = alpha^(254 - (slot + pad)) */
+
+#pragma unroll
+        for (int k = 0; k < RS_NR / 4; ++k)
+            asm volatile("" : "+v"(pk[k]));
+        /* stage 1: b_i ^= X_k b_(i-1), i descending (each log taken of the old b_(i-1)) */
+        static_for<0, RS_NR - 1, 1>([&](auto kc) __attribute__((always_inline)) {
+            constexpr int k = decltype(kc)::value;
+            const uint32_t xs = 128u * (RS_NN - 1u - (slot(k) + pad)); /* plain scaled log X_k */
+            static_for<0, RS_NR - 1 - k, 1>([&](auto jc) __attribute__((always_inline)) {
+                constexpr int j = decltype(jc)::value, i = RS_NR - 1 - j;
+                hb[i] ^= shl7(gf.expa(gf.logh(hb[i - 1]) + xs));
+                if constexpr ((j & 7) == 7)
+                    __builtin_amdgcn_sched_barrier(0); /* eight terms at a time: registers */
+            });
+            __builtin_amdgcn_sched_barrier(0); /* one pass at a time: registers */
+        });
+        /* stage 2: b_i /= X_i ^ X_(i-k-1) for i > k, then b_i ^= b_(i+1) ascending */
+        static_for<0, RS_NR - 1, 1>([&](auto qc) __attribute__((always_inline)) {
+            constexpr int k = RS_NR - 2 - decltype(qc)::value;
+            static_for<k + 1, RS_NR, 1>([&](auto ic) __attribute__((always_inline)) {
+                constexpr int i = decltype(ic)::value;
+                const uint32_t hd = __builtin_amdgcn_bitop3_b32(hx[i], hx[i - k - 1], hz, 0xBE); /* (A ^ B) | C */
+                const uint32_t e = gf.expa(gf.logh(hb[i]) - gf.logh(hd) + pofs + 255u * 128u);
+                hb[i] = hz | shl7(e);
+                if constexpr (((i - k) & 7) == 0)
+                    __builtin_amdgcn_sched_barrier(0); /* eight divisions at a time: registers */
+            });
+            static_for<k, RS_NR - 1, 1>([&](auto ic) __attribute__((always_inline)) {
+                constexpr int i = decltype(ic)::value;
+                hb[i] = __builtin_amdgcn_bitop3_b32(hb[i], hb[i + 1], hz, 0xBE);
+            });
+            __builtin_amdgcn_sched_barrier(0);
+        });
+
+        /* Y_l = alpha^(log z_l + fcr (slot_l + pad + 1)); z_l = 0: no correction,
+         * not counted.  The slots re-extracted here (opaque): kept from the
+         * start, their 32 bytes spilled */
+#pragma unroll
+        for (int k = 0; k < RS_NR / 4; ++k)
+            asm volatile("" : "+v"(pk[k]));
+        uint32_t ncor = 0, mrec[RS_NR / 4];
+        const uint32_t fcr = P.fcr; /* < 98 here (vfast): (slot + pad + 1) fcr < 2^16 */
+#pragma unroll
+        for (int l = 0; l < RS_NR; ++l) {
+            const uint32_t x = (slot(l) + pad + 1u) * fcr; /* the Chien point 1..255, times fcr */
+            const uint32_t ys = 128u * red((x & 0xffu) + (x >> 8)); /* 128 (x mod 255) */
+            const uint32_t mag = gf.expa(gf.logh(hb[l]) + ys);
+            ncor += hb[l] != hz ? 1u : 0u;
+            if ((l & 3) == 0)
+                mrec[l >> 2] = mag;
+            else
+                mrec[l >> 2] |= mag << (8 * (l & 3));
+        }
+        if (fast) {
+            reinterpret_cast<uint4 *>(recw)[2] = make_uint4(mrec[0], mrec[1], mrec[2], mrec[3]);
+            reinterpret_cast<uint4 *>(recw)[3] = make_uint4(mrec[4], mrec[5], mrec[6], mrec[7]);
+            meta[cw] = (uint8_t)(RS_ST_FAST << 5);
+            ok[cw] = 1;
+            if (corrected)
+                corrected[cw] = (uint8_t)ncor;
+        }
+    }
+}
+
 /* ------------------------------------------------------------------------ */
 /* rs_apply_k: the corrections, src/decode.c:215-226                         */
 /* ------------------------------------------------------------------------ */
@@ -1064,7 +1238,14 @@ extern "C" hipError_t rsk_era(const RsDevTables *tab, const RsCorrParams *prm, c
         return hipSuccess;
     const size_t need = (count + EWG - 1) / EWG, /* persistent: more rounds measured slower for rs_era_k */
                  res = (size_t)(num_cu > 0 ? num_cu : 256) * (ERA_WAVES * 256 / EWG);
-    RS_LAUNCH(rs_era_k, dim3((uint32_t)(need < res ? need : res)), dim3(EWG), 0, stream, tab, *prm, ws->syn, pos8,
-                       pos_stride, cnt, count, ws->ext, ws->meta, ws->list, ws->nlist, ok, corrected, pend);
+#ifndef ERA_BP
+#define ERA_BP 1
+#endif
+    if (ERA_BP)
+        RS_LAUNCH(rs_era_bp_k, dim3((uint32_t)(need < res ? need : res)), dim3(EWG), 0, stream, tab, *prm, ws->syn,
+                  pos8, pos_stride, cnt, count, ws->ext, ws->meta, ws->list, ws->nlist, ok, corrected, pend);
+    else
+        RS_LAUNCH(rs_era_k, dim3((uint32_t)(need < res ? need : res)), dim3(EWG), 0, stream, tab, *prm, ws->syn,
+                  pos8, pos_stride, cnt, count, ws->ext, ws->meta, ws->list, ws->nlist, ok, corrected, pend);
     return hipGetLastError();
 }
