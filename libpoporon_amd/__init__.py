@@ -114,7 +114,7 @@ KERNEL_NAMES = {KERNEL_ENCODE: "rs_lfsr_k<false> (encode)", KERNEL_REMAINDER: "r
                 KERNEL_CORRECT: "rs_correct_k (BM/Chien/Forney)", KERNEL_BM: "rs_bm_k (BM/Omega)",
                 KERNEL_CHIEN: "rs_chien_k (Chien)", KERNEL_FORNEY: "rs_forney_k (Forney)",
                 KERNEL_APPLY: "rs_apply_k (apply)", KERNEL_LIST: "list (rs_list1_k; erasure mode: rs_correct_k)",
-                KERNEL_ERASURE: "rs_era_k (erasure)", KERNEL_SINGLE: "rs_dec1_k (one codeword)"}
+                KERNEL_ERASURE: "rs_era_bp_k (erasure)", KERNEL_SINGLE: "rs_dec1_k (one codeword)"}
 
 _lib = None
 

@@ -1243,7 +1243,7 @@ static bool launch_decode(poporon_t *h, uint8_t *d_data, size_t ds, uint8_t *d_p
     }
     /* erasure batches: records (64 B per codeword in ws.ext) applied
      * block-wise (scattered byte read-modify-writes cost ~0.3 ms per 2^20
-     * codewords with 32 erasures).  u8 slots: rs_era_k for 32 sorted
+     * codewords with 32 erasures).  u8 slots: rs_era_bp_k for 32 sorted
      * erasures (prim 1), the errata kernels (rs_errata.hip) for every other
      * count with or without errors, the general kernel's list for what they
      * hand on; u32 slots: the general kernel for all */

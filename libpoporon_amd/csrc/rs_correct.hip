@@ -768,7 +768,7 @@ __global__ __launch_bounds__(COR_WG) void rs_correct_k(const RsDevTables *__rest
         /* a clean codeword succeeds whatever its erasure count (src/decode.c:468:
          * the syndrome test comes first); a dirty one with more erasures than
          * roots overflows the reference's locator (quirk Q5): refused, as
-         * rs_era_k does */
+         * rs_era_bp_k does */
         bool dirty = false;
 #pragma unroll
         for (int q = 0; q < RS_NR / 4; ++q)
@@ -874,7 +874,7 @@ extern "C" hipError_t rsk_correct_era_rec(const RsDevTables *tab, const RsCorrPa
     return hipGetLastError();
 }
 
-/* the same over the codewords list[0 .. *list_n) that rs_era_k hands on */
+/* the same over the codewords list[0 .. *list_n) that rs_era_bp_k hands on */
 extern "C" hipError_t rsk_correct_era_list(const RsDevTables *tab, const RsCorrParams *prm, size_t count,
                                            const uint8_t *syn, const uint8_t *pos8, size_t pos_stride,
                                            const uint8_t *cnt, uint8_t *ok, uint8_t *corrected, uint8_t *rec,

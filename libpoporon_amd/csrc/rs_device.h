@@ -119,7 +119,7 @@ struct RsCorrParams {
 #define RS_ST_DONE 0u /* ok / corrected written */
 #define RS_ST_FAST 1u /* deg(Lambda) = L <= 16: Chien, then Forney */
 #define RS_ST_LIST 2u /* on the list: the general kernel decodes it */
-#define RS_ST_PEND 3u /* erasure mode: left by rs_era_k for the errata kernels */
+#define RS_ST_PEND 3u /* erasure mode: left by rs_era_bp_k for the errata kernels */
 #define RS_ST_ERRATA 4u /* errata decode: deg(Lambda) = L (deg & 31), Chien and Forney next */
 
 struct RsSplitWs {
@@ -279,7 +279,7 @@ hipError_t rsk_correct_era_rec(const RsDevTables *tab, const RsCorrParams *prm, 
                                const uint8_t *pos8, const uint32_t *pos32, size_t pos_stride, const uint8_t *cnt,
                                uint8_t *ok, uint8_t *corrected, uint8_t *rec, uint8_t *meta, int num_cu,
                                hipStream_t stream);
-/* the 32-sorted-erasure kernel (rs_fast.hip: rs_era_k, prim 1, 16-byte
+/* the 32-sorted-erasure kernel (rs_fast.hip: rs_era_bp_k, prim 1, 16-byte
  * aligned u8 slots): records (ws.ext) for its codewords, clean ones finished,
  * the rest RS_ST_PEND for the errata kernels (pend != 0) or onto ws.list
  * (zeroed by rsk_syndrome_reset) for rsk_correct_era_list */

@@ -10,7 +10,7 @@
  *   rs_forney32_k  magnitudes (:159-191) as 64-byte records: root n (in the
  *                  reference's ascending order) with list slot n (:211-214)
  *
- * then rs_apply_k<32> (rs_fast.hip) XORs the records in.  rs_era_k serves
+ * then rs_apply_k<32> (rs_fast.hip) XORs the records in.  rs_era_bp_k serves
  * the one case with its own closed form (32 sorted erasures, prim 1); this
  * path serves the rest: 1..31 erasures with or without errors, unsorted or
  * repeated slots, and the zero-count erasure mode (quirk Q3).
@@ -73,7 +73,7 @@ __global__ __launch_bounds__(XWG, 4) void rs_ebm_k(const RsDevTables *__restrict
                                                   uint8_t *__restrict__ ok, uint8_t *__restrict__ corrected,
                                                   uint32_t only_pend)
 {
-    if (only_pend && nlist[1] == 0u) /* rs_era_k decoded every codeword */
+    if (only_pend && nlist[1] == 0u) /* rs_era_bp_k decoded every codeword */
         return;
     __shared__ uint32_t lgf[512 * 32];
     fill_gfa<XWG>(lgf, T);
@@ -348,7 +348,7 @@ __global__ __launch_bounds__(XWG, 4) void rs_chien32_k(const RsDevTables *__rest
                                                       uint8_t *__restrict__ ok, uint8_t *__restrict__ corrected,
                                                       const uint32_t *__restrict__ npend)
 {
-    if (npend && *npend == 0u) /* rs_era_k decoded every codeword */
+    if (npend && *npend == 0u) /* rs_era_bp_k decoded every codeword */
         return;
     __shared__ uint4 lch[256 * 32];
     for (uint32_t t = threadIdx.x; t < 256u * 32u; t += XWG)
@@ -508,7 +508,7 @@ __global__ __launch_bounds__(XWG, 4) void rs_chien32_k(const RsDevTables *__rest
 /*
  * Root b of the list (newest first) is the reference's root n = deg - 1 - b;
  * num = sum_(m < deg) Omega_m alpha^(i m) and den = sum_h Lambda_(2h+1)
- * alpha^(2h i) (src/decode.c:159-191), each split at m = 16 as rs_era_k's,
+ * alpha^(2h i) (src/decode.c:159-191), each split at m = 16 as rs_era_k's (round 3),
  * magnitude alpha^(log num + log alpha^(i (fcr-1)) + 255 - log den) (no den =
  * 0 guard, as the reference); a zero numerator corrects nothing and is not
  * counted.  The record pairs magnitude b with list slot deg - 1 - b: the
@@ -522,7 +522,7 @@ __global__ __launch_bounds__(XWG, 4) void rs_forney32_k(const RsDevTables *__res
                                                        uint8_t *__restrict__ meta, uint8_t *__restrict__ ok,
                                                        uint8_t *__restrict__ corrected, const uint32_t *__restrict__ npend)
 {
-    if (npend && *npend == 0u) /* rs_era_k decoded every codeword */
+    if (npend && *npend == 0u) /* rs_era_bp_k decoded every codeword */
         return;
     __shared__ uint32_t lgf[512 * 32];
     fill_gfa<XWG>(lgf, T);

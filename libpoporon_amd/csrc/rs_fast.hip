@@ -597,7 +597,7 @@ __global__ __launch_bounds__(F2WG, 6) void rs_forney_k(const RsDevTables *__rest
 }
 
 /* ------------------------------------------------------------------------ */
-/* rs_era_k: erasure decode at num_roots known positions (configs[3])       */
+/* rs_era_bp_k: erasure decode at num_roots known positions (configs[3])    */
 /* ------------------------------------------------------------------------ */
 
 /*
@@ -607,284 +607,15 @@ __global__ __launch_bounds__(F2WG, 6) void rs_forney_k(const RsDevTables *__rest
  * prod(1 + X_l x) of :31-47, X_l = alpha^(254 - L_l), L_l = slot + pad, of
  * degree 32 (every X_l nonzero).  Its roots are the Chien points (:117-141)
  * i_l = L_l + 1, found in ascending order = slot order, so magnitude l goes
- * to slot l (:211-214), and the count equals the degree.  Forney (:147-191)
- * runs at those points; the re-syndrome check (:193-209) passes by
- * construction (32 equations, 32 unknowns, distinct X_l).  Lambda_32 plays
- * no part (Omega stops at x^31, Lambda' at x^30).  Everything else -- other
- * counts, unsorted or repeated slots, slots past the codeword -- goes to the
- * list (rs_correct_k in record mode).  Output: the 64-byte record of
- * rs_apply_k<32> (slots, magnitudes).
- *
- * Registers: the locator halves, then Lambda's and the syndromes' logs one
- * register each for Omega (64 registers: plain adds instead of half-rate SDWA
- * word selects, 2 %, profiles/r03_era_unpacked_ab.log); Forney reads Omega
- * and the odd Lambda terms unpacked (48 registers, 4 waves/SIMD, 128 VGPRs:
- * the kernel is issue-bound, occupancy 4, 6 and 8 measured the same) and splits each
- * sum at m = 16, so one 16-step power chain per root serves both halves
- * (0.36 -> 0.31-0.33 ms, profiles/r03_era_experiments.log); slots are
- * re-read where needed.
+ * to slot l (:211-214), and the count equals the degree.  Everything else --
+ * other counts, unsorted or repeated slots, slots past the codeword -- is
+ * left to the errata kernels (RS_ST_PEND) or goes to the list (rs_correct_k
+ * in record mode).  Output: the 64-byte record of rs_apply_k<32> (slots,
+ * magnitudes).  The round-3 kernel that ran the locator, Omega and Forney
+ * here: tools/experiments/rs_era_forney_k.hip.txt.
  */
-#define EWG 1024 /* rs_era_k: 4 waves/SIMD; 6 (768-thread groups) and 8 measured the same: issue-bound (profiles/r03_era_experiments.log) */
-#define ERA_WAVES 4
-#define ERA_R 4 /* Forney roots per step: one record dword */
-#define ERA_OG 8 /* Omega lookups per group */
-
-__global__ __launch_bounds__(EWG, ERA_WAVES) void rs_era_k(const RsDevTables *__restrict__ T, RsCorrParams P,
-                                                         const uint8_t *__restrict__ syn,
-                                                         const uint8_t *__restrict__ pos8, size_t pos_stride,
-                                                         const uint8_t *__restrict__ cntp, size_t count,
-                                                         uint8_t *__restrict__ rec, uint8_t *__restrict__ meta,
-                                                         uint32_t *__restrict__ list, uint32_t *__restrict__ nlist,
-                                                         uint8_t *__restrict__ ok, uint8_t *__restrict__ corrected,
-                                                         uint32_t pend)
-{
-    __shared__ uint32_t lgf[512 * 32];
-    fill_gfa<EWG>(lgf, T);
-    __syncthreads();
-    const GfA gf{lds_addr(lgf) + 4u * (threadIdx.x & 31u) + 1u};
-    const uint32_t pofs = gf.pofs;
-    const uint32_t mp = 255u * 128u + pofs; /* alpha^(log a - log b) = expa(loga a - loga b + mp) */
-    const uint32_t lim = P.size + RS_NR, pad = (uint32_t)P.pad;
-
-    uint32_t it = 0;
-    for (size_t base = (size_t)blockIdx.x * EWG; base < count; base += (size_t)gridDim.x * EWG, ++it) {
-        prio_by_progress(it);
-        const size_t cw = base + threadIdx.x;
-        const bool valid = cw < count;
-        uint4 sa = make_uint4(0, 0, 0, 0), sb = sa, pa = sa, pb = sa;
-        uint32_t ne = 0;
-        const uint8_t *slots = pos8 + (valid ? cw : 0) * pos_stride;
-        if (valid) {
-            sa = reinterpret_cast<const uint4 *>(syn)[2 * cw];
-            sb = reinterpret_cast<const uint4 *>(syn)[2 * cw + 1];
-            pa = reinterpret_cast<const uint4 *>(slots)[0];
-            pb = reinterpret_cast<const uint4 *>(slots)[1];
-            ne = cntp[cw];
-        }
-        const bool any = (sa.x | sa.y | sa.z | sa.w | sb.x | sb.y | sb.z | sb.w) != 0u;
-        uint32_t pk[RS_NR / 4] = {pa.x, pa.y, pa.z, pa.w, pb.x, pb.y, pb.z, pb.w};
-        bool asc = true;
-        uint32_t prev = pk[0] & 0xffu;
-#pragma unroll
-        for (int n = 1; n < RS_NR; ++n) {
-            const uint32_t p = (pk[n >> 2] >> (8 * (n & 3))) & 0xffu;
-            asc = asc && p > prev;
-            prev = p;
-        }
-        const bool fast = valid && any && ne == RS_NR && asc && prev < lim;
-        if (valid && !fast) {
-            if (!any) {
-                ok[cw] = 1;
-                if (corrected)
-                    corrected[cw] = 0;
-                meta[cw] = (uint8_t)(RS_ST_DONE << 5);
-            } else if (pend) { /* the errata kernels (rs_errata.hip) decode it */
-                meta[cw] = (uint8_t)(RS_ST_PEND << 5);
-            } else {
-                meta[cw] = (uint8_t)(RS_ST_LIST << 5);
-                list[atomicAdd(nlist, 1u)] = (uint32_t)cw;
-            }
-        }
-        const uint64_t pw = __ballot(valid && any && !fast && pend);
-        if (pw != 0ull && (threadIdx.x & 63u) == (uint32_t)__builtin_ctzll(pw))
-            nlist[1] = 1u; /* the errata kernels run only if some codeword is pending: one store per wave */
-        if (__ballot(fast) == 0ull) /* uniform */
-            continue;
-        uint32_t *recw = reinterpret_cast<uint32_t *>(rec + (valid ? cw : 0) * 64u);
-        if (fast) { /* the record's slots now: pa / pb need no registers past the locator */
-            reinterpret_cast<uint4 *>(recw)[0] = pa;
-            reinterpret_cast<uint4 *>(recw)[1] = pb;
-        }
-        if (!fast) { /* lanes along for the ride: any in-range slots */
-#pragma unroll
-            for (int k = 0; k < RS_NR / 4; ++k)
-                pk[k] = 0;
-        }
-
-        /* ---- erasure locator, src/decode.c:31-47, as the product of two
-         * halves A = prod_(l<16), B = prod_(l>=16) (the same field elements;
-         * fewer lookups than one 32-factor product).  Each half
-         * incrementally: H_j += X_l H_(j-1), j = l+1 down to 1 ---- */
-        constexpr int NH = RS_NR / 2;
-        auto half_locator = [&](uint32_t (&h)[NH + 1], auto l0c) __attribute__((always_inline)) {
-            constexpr int L0 = decltype(l0c)::value;
-            /* coefficients as log-entry addresses (GfA::hz): a term is the log
-             * of the old H_(j-1) (ds_read_u16) and the exp of the product, two
-             * lookups; the logs once at the end */
-            const uint32_t HZ = gf.hz();
-            h[0] = HZ + 128u;
-#pragma unroll
-            for (int j = 1; j <= NH; ++j)
-                h[j] = HZ;
-            static_for<0, NH, 1>([&](auto lc) __attribute__((always_inline)) {
-                constexpr int l = decltype(lc)::value, lg = L0 + l;
-                const uint32_t p = (pk[lg >> 2] >> (8 * (lg & 3))) & 0xffu;
-                const uint32_t xs = 128u * (254u - (p + pad)); /* scaled log X_l */
-                static_for<0, l + 1, 1>([&](auto kc) __attribute__((always_inline)) {
-                    constexpr int j = l + 1 - decltype(kc)::value;
-                    h[j] ^= shl7(gf.expa((j == 1 ? pofs : gf.logh(h[j - 1])) + xs));
-                    if constexpr ((j & 7) == 0)
-                        __builtin_amdgcn_sched_barrier(0); /* eight terms at a time: registers */
-                });
-                __builtin_amdgcn_sched_barrier(0); /* one factor at a time: registers */
-            });
-            h[0] = pofs;
-#pragma unroll
-            for (int j = 1; j <= NH; ++j)
-                h[j] = gf.logh(h[j]);
-        };
-        uint32_t ha[NH + 1], hb[NH + 1]; /* address-form logs of A_0..16, B_0..16 */
-        half_locator(ha, std::integral_constant<int, 0>{});
-        half_locator(hb, std::integral_constant<int, NH>{});
-#pragma unroll
-        for (int j = 0; j <= NH; ++j)
-            hb[j] -= pofs; /* plain scaled logs (zero: SZ) */
-        /* Lambda_k = sum_(i+j=k) A_i B_j, k < 32 (Lambda_32 plays no part) */
-        uint32_t alu[RS_NR]; /* address-form logs of Lambda_0..31 (one register each: plain adds below) */
-        static_for<0, RS_NR, 1>([&](auto kc) __attribute__((always_inline)) {
-            constexpr int k = decltype(kc)::value;
-            uint32_t o = pofs;
-            if constexpr (k > 0) {
-                uint32_t acc = 0;
-#pragma unroll
-                for (int i = (k > NH ? k - NH : 0); i <= (k < NH ? k : NH); ++i)
-                    acc ^= gf.expa(ha[i] + hb[k - i]);
-                asm volatile("" : "+v"(acc));
-                o = gf.loga(acc);
-            }
-            alu[k] = o;
-            __builtin_amdgcn_sched_barrier(0); /* one coefficient at a time: registers */
-        });
-
-        /* ---- Omega = S Lambda mod x^32, src/decode.c:147-158 ---- */
-        uint32_t slu[RS_NR]; /* plain scaled logs of S_0..31 */
-        {
-            /* the syndromes again (L2): keeping them through the locator costs registers */
-            const uint8_t *sp = syn + (valid ? cw : 0) * RS_NR;
-            asm volatile("" : "+v"(sp));
-            sa = reinterpret_cast<const uint4 *>(sp)[0];
-            sb = reinterpret_cast<const uint4 *>(sp)[1];
-            const uint32_t sw[8] = {sa.x, sa.y, sa.z, sa.w, sb.x, sb.y, sb.z, sb.w};
-#pragma unroll
-            for (int k = 0; k < RS_NR; ++k)
-                slu[k] = gf.logs((sw[k >> 2] >> (8 * (k & 3))) & 0xffu);
-        }
-        uint32_t ob[RS_NR / 4]; /* byte logs of Omega_0..31 (255 = zero), four per register */
-        static_for<0, RS_NR, 1>([&](auto mc) __attribute__((always_inline)) {
-            constexpr int m = decltype(mc)::value;
-            uint32_t acc = 0;
-            static_for<0, m + 1, ERA_OG>([&](auto gc) __attribute__((always_inline)) {
-                constexpr int g = decltype(gc)::value; /* eight lookups at a time: registers */
-#pragma unroll
-                for (int t = g; t <= m && t < g + ERA_OG; ++t)
-                    acc ^= gf.expa(alu[t] + slu[m - t]);
-                asm volatile("" : "+v"(acc)); /* the sum now: no deferred xor tree */
-                __builtin_amdgcn_sched_barrier(0);
-            });
-            const uint32_t o = gf.plog(gf.loga(acc));
-            if constexpr ((m & 3) == 0)
-                ob[m >> 2] = o;
-            else
-                ob[m >> 2] |= o << (8 * (m & 3));
-            __builtin_amdgcn_sched_barrier(0); /* one coefficient's lookups at a time: registers */
-        });
-
-        /* ---- Forney at the known roots, src/decode.c:159-191: num = sum_m
-         * Omega_m alpha^(i m), den = sum_h Lambda_(2h+1) alpha^(2h i),
-         * magnitude alpha^(log num + log alpha^(i (fcr-1)) + 255 - log den);
-         * a zero numerator corrects nothing and is not counted ---- */
-        uint32_t ncor = 0, mrec[RS_NR / 4];
-        const uint32_t *slw = reinterpret_cast<const uint32_t *>(slots);
-        uint32_t opu[RS_NR], alou[RS_NR / 2]; /* unpacked: plain adds in the loop, not SDWA word selects */
-#pragma unroll
-        for (int m = 0; m < RS_NR; ++m)
-            opu[m] = gf.afrom((ob[m >> 2] >> (8 * (m & 3))) & 0xffu);
-#pragma unroll
-        for (int h = 0; h < RS_NR / 2; ++h)
-            alou[h] = alu[2 * h + 1];
-#pragma unroll 1
-        for (uint32_t q = 0; q < RS_NR / ERA_R; ++q) {
-            uint32_t w[ERA_R / 4];
-#pragma unroll
-            for (int k = 0; k < ERA_R / 4; ++k)
-                w[k] = fast ? slw[q * (ERA_R / 4) + k] : 0u;
-            uint32_t ii[ERA_R], si[ERA_R], s[ERA_R], num[ERA_R], den[ERA_R];
-#pragma unroll
-            for (int t = 0; t < ERA_R; ++t) {
-                ii[t] = ((w[t >> 2] >> (8 * (t & 3))) & 0xffu) + pad + 1u; /* the Chien point, 1..255 */
-                si[t] = 128u * (ii[t] == 255u ? 0u : ii[t]);
-                s[t] = 0;
-                num[t] = 0;
-                den[t] = 0;
-            }
-            /* m = 16 a + b: num = N_0 + alpha^(16 i) N_1, N_a = sum_b Omega_(16a+b)
-             * alpha^(b i), and den likewise over the even b: one power chain
-             * of 16 steps per root instead of 32 */
-            uint32_t nh[ERA_R], dh[ERA_R];
-#pragma unroll
-            for (int t = 0; t < ERA_R; ++t)
-                nh[t] = dh[t] = 0;
-#pragma unroll
-            for (int b = 0; b < RS_NR / 2; ++b) {
-#pragma unroll
-                for (int t = 0; t < ERA_R; ++t) {
-                    num[t] ^= gf.expa(opu[b] + s[t]);
-                    nh[t] ^= gf.expa(opu[b + 16] + s[t]);
-                    if ((b & 1) == 0) {
-                        den[t] ^= gf.expa(alou[b >> 1] + s[t]);
-                        dh[t] ^= gf.expa(alou[(b >> 1) + 8] + s[t]);
-                    }
-                    s[t] = addmod7(s[t], si[t]);
-                }
-                if (b & 1) {
-#pragma unroll
-                    for (int t = 0; t < ERA_R; ++t)
-                        asm volatile("" : "+v"(num[t]), "+v"(den[t]), "+v"(nh[t]), "+v"(dh[t]));
-                    __builtin_amdgcn_sched_barrier(0); /* two powers at a time: registers */
-                }
-            }
-#pragma unroll
-            for (int t = 0; t < ERA_R; ++t) { /* s = 128 (16 i mod 255) */
-                num[t] ^= gf.expa(gf.loga(nh[t]) + s[t]);
-                den[t] ^= gf.expa(gf.loga(dh[t]) + s[t]);
-            }
-            uint32_t cur[ERA_R / 4] = {};
-#pragma unroll
-            for (int t = 0; t < ERA_R; ++t) {
-                /* alpha^(log num + ln2 + 255 - log den) from the address forms
-                 * (den != 0 at the distinct erasure locations), reduced once */
-                const uint32_t l2s = P.fcr == 1u ? 0u
-                                                 : 128u * mod255((uint32_t)((int32_t)ii[t] * ((int32_t)P.fcr - 1) +
-                                                                            (int32_t)RS_NN));
-                const uint32_t x = gf.loga(num[t]) - gf.loga(den[t]) + mp + l2s;
-                const bool z = num[t] != 0u;
-                ncor += z ? 1u : 0u;
-                cur[t >> 2] |= (z ? gf.expa(min(x, x - 255u * 128u)) : 0u) << (8 * (t & 3));
-            }
-            /* magnitude words through a shift register: the record's 32
-             * bytes go out as two 16-byte stores (eight dword stores per
-             * record cost ~130 B of partial-line writes per codeword) */
-#pragma unroll
-            for (int k = 0; k < RS_NR / 4 - ERA_R / 4; ++k)
-                mrec[k] = mrec[k + ERA_R / 4];
-#pragma unroll
-            for (int k = 0; k < ERA_R / 4; ++k)
-                mrec[RS_NR / 4 - ERA_R / 4 + k] = cur[k];
-        }
-        if (fast) {
-            reinterpret_cast<uint4 *>(recw)[2] = make_uint4(mrec[0], mrec[1], mrec[2], mrec[3]);
-            reinterpret_cast<uint4 *>(recw)[3] = make_uint4(mrec[4], mrec[5], mrec[6], mrec[7]);
-            meta[cw] = (uint8_t)(RS_ST_FAST << 5);
-            ok[cw] = 1;
-            if (corrected)
-                corrected[cw] = (uint8_t)ncor;
-        }
-    }
-}
-
 /*
- * rs_era_bp_k: the same codewords and output as rs_era_k, with the magnitudes
- * solved directly.  With 32 erasures the 32 syndromes determine them: S_i =
+ * The magnitudes are solved directly.  With 32 erasures the 32 syndromes determine them: S_i =
  * sum_l z_l X_l^i (i < 32, z_l = Y_l X_l^fcr) is a square Vandermonde system
  * with distinct nodes, whatever the syndromes are, and the reference's
  * Forney step (src/decode.c:159-191) computes its unique solution (its
@@ -909,7 +640,13 @@ __global__ __launch_bounds__(EWG, ERA_WAVES) void rs_era_k(const RsDevTables *__
  * (Prototype against the oracle over fcr 0, 1, 2, 5, 97, sizes 223 and 100,
  * extra errors besides the erasures: bit-exact.)
  */
-__global__ __launch_bounds__(EWG, ERA_WAVES) void rs_era_bp_k(const RsDevTables *__restrict__ T, RsCorrParams P,
+#ifndef BPWG
+#define BPWG 1024 /* rs_era_bp_k: 4 waves/SIMD at 120 VGPRs; 5 or 6 (640- / 768-thread groups) spill 14 / 47 */
+#endif
+#ifndef BP_WAVES
+#define BP_WAVES 4
+#endif
+__global__ __launch_bounds__(BPWG, BP_WAVES) void rs_era_bp_k(const RsDevTables *__restrict__ T, RsCorrParams P,
                                                             const uint8_t *__restrict__ syn,
                                                             const uint8_t *__restrict__ pos8, size_t pos_stride,
                                                             const uint8_t *__restrict__ cntp, size_t count,
@@ -919,14 +656,14 @@ __global__ __launch_bounds__(EWG, ERA_WAVES) void rs_era_bp_k(const RsDevTables 
                                                             uint32_t pend)
 {
     __shared__ uint32_t lgf[512 * 32];
-    fill_gfa<EWG>(lgf, T);
+    fill_gfa<BPWG>(lgf, T);
     __syncthreads();
     const GfA gf{lds_addr(lgf) + 4u * (threadIdx.x & 31u) + 1u};
     const uint32_t pofs = gf.pofs, hz = gf.hz();
     const uint32_t lim = P.size + RS_NR, pad = (uint32_t)P.pad;
 
     uint32_t it = 0;
-    for (size_t base = (size_t)blockIdx.x * EWG; base < count; base += (size_t)gridDim.x * EWG, ++it) {
+    for (size_t base = (size_t)blockIdx.x * BPWG; base < count; base += (size_t)gridDim.x * BPWG, ++it) {
         prio_by_progress(it);
         const size_t cw = base + threadIdx.x;
         const bool valid = cw < count;
@@ -1236,16 +973,9 @@ extern "C" hipError_t rsk_era(const RsDevTables *tab, const RsCorrParams *prm, c
 {
     if (count == 0)
         return hipSuccess;
-    const size_t need = (count + EWG - 1) / EWG, /* persistent: more rounds measured slower for rs_era_k */
-                 res = (size_t)(num_cu > 0 ? num_cu : 256) * (ERA_WAVES * 256 / EWG);
-#ifndef ERA_BP
-#define ERA_BP 1
-#endif
-    if (ERA_BP)
-        RS_LAUNCH(rs_era_bp_k, dim3((uint32_t)(need < res ? need : res)), dim3(EWG), 0, stream, tab, *prm, ws->syn,
-                  pos8, pos_stride, cnt, count, ws->ext, ws->meta, ws->list, ws->nlist, ok, corrected, pend);
-    else
-        RS_LAUNCH(rs_era_k, dim3((uint32_t)(need < res ? need : res)), dim3(EWG), 0, stream, tab, *prm, ws->syn,
-                  pos8, pos_stride, cnt, count, ws->ext, ws->meta, ws->list, ws->nlist, ok, corrected, pend);
+    const size_t need = (count + BPWG - 1) / BPWG, /* persistent (more rounds measured slower for rs_era_k) */
+                 res = (size_t)(num_cu > 0 ? num_cu : 256) * (BP_WAVES * 256 / BPWG);
+    RS_LAUNCH(rs_era_bp_k, dim3((uint32_t)(need < res ? need : res)), dim3(BPWG), 0, stream, tab, *prm, ws->syn,
+              pos8, pos_stride, cnt, count, ws->ext, ws->meta, ws->list, ws->nlist, ok, corrected, pend);
     return hipGetLastError();
 }

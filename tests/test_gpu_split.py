@@ -216,7 +216,7 @@ def test_split_erasures_vs_oracle(monkeypatch, oracle_default, path, size, dup):
 
 
 def test_split_erasure_kernels_timed(monkeypatch, torch_cuda_split):
-    """A 2^16 batch with 32 sorted erasures each: remainder, rs_era_k, the
+    """A 2^16 batch with 32 sorted erasures each: remainder, rs_era_bp_k, the
     (empty) list, block apply -- codewords restored, 32 corrections each."""
     torch = torch_cuda_split
     h = _handle(monkeypatch, "split")
@@ -250,7 +250,7 @@ def test_split_erasure_kernels_timed(monkeypatch, torch_cuda_split):
 @pytest.mark.parametrize("params", [(8, 0x11D, 0, 1, 32), (8, 0x187, 5, 1, 32), (8, 0x11D, 1, 2, 32),
                                     (8, 0x11D, 5, 7, 32)])
 def test_split_erasures_other_parameters_vs_oracle(monkeypatch, params):
-    """Erasure batches under other fcr / prim / field polynomials: rs_era_k
+    """Erasure batches under other fcr / prim / field polynomials: rs_era_bp_k
     (prim 1, any fcr) and the record-mode general kernel (prim != 1)."""
     from oracle import Oracle
     o = Oracle(*params)
@@ -269,7 +269,7 @@ def test_erasure_count_past_roots(monkeypatch, oracle_default, path):
     the locator is built): a clean codeword succeeds with 0 corrections
     whatever its count (src/decode.c:468 tests the syndromes first), a dirty
     one is refused (ok 0, bytes untouched) -- the same answer on the split
-    path (rs_era_k + list) and the single kernel, mixed with in-range
+    path (rs_era_bp_k + list) and the single kernel, mixed with in-range
     codewords in every wave."""
     h = _handle(monkeypatch, path)
     rng = np.random.default_rng(4242)
@@ -346,7 +346,7 @@ def test_errata_vs_oracle(monkeypatch, oracle_default, path, size, ne, nerr, sor
 
 def test_errata_kernels_timed(monkeypatch, torch_cuda_split):
     """2^16 codewords with 16 sorted erasures and 8 errors each on the device
-    API: rs_era_k leaves them pending, the errata kernels decode them, the
+    API: rs_era_bp_k leaves them pending, the errata kernels decode them, the
     general kernel never runs; ok / corrected for all, bytes of a sample
     against the oracle."""
     torch = torch_cuda_split
@@ -393,7 +393,7 @@ def test_errata_kernels_timed(monkeypatch, torch_cuda_split):
 
 @pytest.mark.parametrize("stride", [32, 40, 33])
 def test_errata_slot_strides(monkeypatch, oracle_default, torch_cuda_split, stride):
-    """Slot rows 32 (rs_era_k + errata), 40 (errata alone: not 16-byte rows)
+    """Slot rows 32 (rs_era_bp_k + errata), 40 (errata alone: not 16-byte rows)
     and 33 bytes apart (unaligned rows: the general kernel) give the same
     answers, equal to the oracle's."""
     torch = torch_cuda_split
