@@ -31,7 +31,7 @@ for step in "$@"; do
     ab) # A/B of the experiment builds in build/*.so, alternated twice (same box)
         run ab 900 python tools/exp_bench.py $(ls build/*.so) $(ls build/*.so) ;;
     prof) run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- \
-        python3 bench.py --no-cpu-baseline --no-host --no-c4 --no-latency --steps 10 ;;
+        python3 bench.py --no-cpu-baseline --no-host --no-c4 --no-latency --no-mixed --steps 10 ;;
     pmc)
         # one rocprofv3 pass per counter group (never combined with tracing)
         i=0
@@ -46,7 +46,7 @@ for step in "$@"; do
     traffic)
         # HBM bytes per codeword of each bench path: FETCH_SIZE and WRITE_SIZE
         # in separate passes per driver mode (tools/pmc_traffic.py)
-        for mode in roundtrip erasure errata; do
+        for mode in roundtrip erasure errata mixed; do
             for c in FETCH_SIZE WRITE_SIZE; do
                 lc=$(echo $c | cut -d_ -f1 | tr A-Z a-z)
                 run traffic_${mode}_$lc 150 rocprofv3 --pmc $c -d gpurun_out/traffic/${mode}_$lc -o pmc \

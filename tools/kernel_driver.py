@@ -27,7 +27,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--n", type=int, default=1 << 20)
     ap.add_argument("--reps", type=int, default=5)
-    ap.add_argument("--mode", default="roundtrip", choices=["roundtrip", "erasure", "errata"])
+    ap.add_argument("--mode", default="roundtrip", choices=["roundtrip", "erasure", "errata", "mixed"])
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     rs = P.Poporon.default(device=0)
@@ -49,6 +49,12 @@ def main():
         cnt = torch.full((a.n,), 32, dtype=torch.uint8, device=dev)
         kw = dict(d_positions=slots.data_ptr(), positions_stride=32, d_counts=cnt.data_ptr())
         want = 32
+    elif a.mode == "mixed":  # bench.py decode_mixed: binomial(255, 0.045) errors per codeword, capped at 24
+        pos, mag = devdata.synth_errors(bench.SEED + 10, 0, a.n, bench.MIXED_CAP, N, dev)
+        ne = torch.from_numpy(bench.mixed_counts(0, a.n)).to(dev)
+        mag = mag * (torch.arange(bench.MIXED_CAP, device=dev)[None, :] < ne[:, None].long()).to(mag.dtype)
+        kw = {}
+        want = None
     else:  # bench.py errata16e8: 24 sorted positions, every third an error, the rest 16 erasure slots
         pos, mag = devdata.synth_errors(bench.SEED + 9, 0, a.n, 24, K, dev)
         pos = pos.sort(dim=1).values
@@ -73,6 +79,9 @@ def main():
         d = bad[r].data_ptr()
         rs.decode_batch_device(d, N, d + K, N, K, a.n, ok.data_ptr(), cor.data_ptr(), stream=s, **kw)
     torch.cuda.synchronize()
+    if want is None:  # mixed: the codewords past t fail or miscorrect as the reference does
+        print("driver ok", a.mode, a.n, a.reps, "ok", int(ok.sum()))
+        return
     assert int(ok.sum()) == a.n and bool((cor == want).all()), "decode failures"
     if a.mode != "errata":  # errata: the reference applies root n's magnitude at slot n (not restored)
         assert all(bool((x == cw).all()) for x in bad + enc), "decoded bytes differ"

@@ -4,7 +4,7 @@
     python tools/pmc_traffic.py gpurun_out/traffic --json profiles/traffic_latest.json
 
 Expects <dir>/<mode>_fetch/*counter_collection.csv and <dir>/<mode>_write/...
-for mode in {roundtrip, erasure, errata}: one `rocprofv3 --pmc FETCH_SIZE` and one
+for mode in {roundtrip, erasure, errata, mixed}: one `rocprofv3 --pmc FETCH_SIZE` and one
 `--pmc WRITE_SIZE` pass (never together with tracing; tools/gpu_session.sh
 step `traffic`) over `tools/kernel_driver.py --mode <mode> --n N`.
 
@@ -38,8 +38,8 @@ PATTERNS = [
     (r"rs_lfsr_k<0,", bench.K_ENCODE), (r"rs_lfsr_k<1,", bench.K_REMAINDER),
     (r"\brs_bm_k\b|\brs_ebm_k\b", bench.K_BM), (r"\brs_chien_k\b|\brs_chien32_k\b", bench.K_CHIEN),
     (r"rs_forney_k|rs_forney32_k", bench.K_FORNEY),
-    (r"rs_apply_k", bench.K_APPLY), (r"\brs_era_k\b", bench.K_ERASURE),
-    (r"rs_correct_k<[^>]*true>|rs_correct_list|rs_correct_k", bench.K_LIST),
+    (r"rs_apply_k", bench.K_APPLY), (r"\brs_era_bp_k\b|\brs_era_k\b", bench.K_ERASURE),
+    (r"\brs_list1_k\b|rs_correct_k<[^>]*true>|rs_correct_list|rs_correct_k", bench.K_LIST),
 ]
 
 
@@ -69,7 +69,8 @@ def main():
     ap.add_argument("--n", type=int, default=1 << 20, help="codewords per dispatch (kernel_driver --n)")
     ap.add_argument("--json", default=None)
     a = ap.parse_args()
-    runs = {"encode": "roundtrip", "decode16": "roundtrip", "erasure32": "erasure", "errata16e8": "errata"}
+    runs = {"encode": "roundtrip", "decode16": "roundtrip", "erasure32": "erasure", "errata16e8": "errata",
+            "decode_mixed": "mixed"}
     out = {"source_stamp": bench.source_stamp(), "date": datetime.datetime.utcnow().strftime("%Y-%m-%d %H:%M UTC"),
            "codewords_per_dispatch": a.n,
            "note": "hbm bytes = FETCH_SIZE x 1024 x 2 + WRITE_SIZE x 1024 per dispatch (MI355X_MICROARCH.md HBM; the "
