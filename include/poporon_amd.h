@@ -135,16 +135,18 @@ bool poporon_decode_batch(poporon_t *pprn, uint8_t *data, size_t data_stride, ui
  * returns the summed kernel time (ms) and launch count for one kernel id:
  * 0 = encode LFSR, 1 = remainder LFSR, 2 = correction (single kernel),
  * 3 = check LFSR; the split error-mode decode of large batches: 4 = BM +
- * Omega, 5 = Chien, 6 = Forney, 8 = apply, 7 = the general kernel over the
- * codewords the split kernels hand on.  Erasure-mode batches of that size:
- * 1, 9 = the locator / Omega / Forney kernel for 32 sorted erasures (prim 1),
- * 7 = the general kernel over the rest (records), 8 = apply.  A batch of
- * one codeword (and every poporon_decode / poporon_encode call): 10 = the
- * one-workgroup decoder (rs_dec1_k), 0 = encode (rs_enc1_k).
+ * Omega, 5 = Chien, 6 = Forney, 8 = apply, 7 = the one-codeword-per-wave
+ * decoder over the codewords the split kernels hand on.  Erasure-mode
+ * batches of that size: 1, 9 = the 32-sorted-erasure kernel (prim 1), 4 / 5
+ * / 6 = the errata kernels, 7 = the same per-wave decoder over the rest, 8 =
+ * apply.  A batch of one codeword: 10 = the one-workgroup decoder
+ * (rs_dec1_k), 0 = encode (rs_enc1_k).  Batches of 2..8191 codewords: 11 =
+ * the one-codeword-per-wave decoder (rs_wave_k, syndromes included).
  *
- * Error-mode batches of at least 8192 codewords (no erasures, no external
- * syndromes) take the split decode; POPORON_AMD_DECODE_PATH=split / single
- * in the environment at poporon_create forces one or the other. */
+ * Error- and erasure-mode batches of at least 8192 codewords take the split
+ * decode; POPORON_AMD_DECODE_PATH=split / single / wave in the environment
+ * at poporon_create forces the split kernels, the lane-per-codeword general
+ * kernel (rs_correct_k) or the per-wave decoder for every batch size. */
 #define POPORON_AMD_KERNEL_ENCODE 0
 #define POPORON_AMD_KERNEL_REMAINDER 1
 #define POPORON_AMD_KERNEL_CORRECT 2
@@ -156,6 +158,7 @@ bool poporon_decode_batch(poporon_t *pprn, uint8_t *data, size_t data_stride, ui
 #define POPORON_AMD_KERNEL_APPLY 8
 #define POPORON_AMD_KERNEL_ERASURE 9
 #define POPORON_AMD_KERNEL_SINGLE 10
+#define POPORON_AMD_KERNEL_WAVE 11
 bool poporon_amd_timing(poporon_t *pprn, int enable);
 bool poporon_amd_timing_read(poporon_t *pprn, int kernel, double *total_ms, uint64_t *launches);
 

@@ -110,11 +110,13 @@ _SIGS = {
 # kernel ids for poporon_amd_timing_read (include/poporon_amd.h)
 KERNEL_ENCODE, KERNEL_REMAINDER, KERNEL_CORRECT = 0, 1, 2
 KERNEL_BM, KERNEL_CHIEN, KERNEL_FORNEY, KERNEL_LIST, KERNEL_APPLY, KERNEL_ERASURE, KERNEL_SINGLE = 4, 5, 6, 7, 8, 9, 10
+KERNEL_WAVE = 11
 KERNEL_NAMES = {KERNEL_ENCODE: "rs_lfsr_k<false> (encode)", KERNEL_REMAINDER: "rs_lfsr_k<true> (remainder)",
                 KERNEL_CORRECT: "rs_correct_k (BM/Chien/Forney)", KERNEL_BM: "rs_bm_k (BM/Omega)",
                 KERNEL_CHIEN: "rs_chien_k (Chien)", KERNEL_FORNEY: "rs_forney_k (Forney)",
-                KERNEL_APPLY: "rs_apply_k (apply)", KERNEL_LIST: "list (rs_list1_k; erasure mode: rs_correct_k)",
-                KERNEL_ERASURE: "rs_era_bp_k (erasure)", KERNEL_SINGLE: "rs_dec1_k (one codeword)"}
+                KERNEL_APPLY: "rs_apply_k (apply)", KERNEL_LIST: "rs_wave_k (list)",
+                KERNEL_ERASURE: "rs_era_bp_k (erasure)", KERNEL_SINGLE: "rs_dec1_k (one codeword)",
+                KERNEL_WAVE: "rs_wave_k (small batch)"}
 
 _lib = None
 

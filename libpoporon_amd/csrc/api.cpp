@@ -106,7 +106,7 @@ struct _poporon_config_t {
     uint8_t correction_capability; /* BCH */
 };
 
-#define NKERN 11
+#define NKERN 12
 struct TimedLaunch {
     int kernel;
     hipEvent_t a, b;
@@ -170,7 +170,8 @@ struct _poporon_t {
     size_t last_corrected;
     bool supported; /* fast || generic */
     bool fast;      /* served by the RS(255,223) kernels (rs_kernels.hip, rs_correct.hip) */
-    int decode_path; /* 0: by batch size, 1: split kernels (rs_fast.hip), 2: single kernel */
+    int decode_path; /* 0: by batch size, 1: split kernels (rs_fast.hip), 2: single kernel (rs_correct_k),
+                      * 3: one codeword per wave (rs_wave_k) */
     bool generic;   /* served by the general-parameter kernels (rs_generic.hip) */
     RsDevTables host_tab;
     RsCorrParams corr;
@@ -525,7 +526,7 @@ static void build_tables(poporon_t *h)
     const char *fv = getenv("POPORON_AMD_FORCE_VERIFY");
     p.force_verify = (fv && fv[0] == '1') ? 1u : 0u;
     const char *dp = getenv("POPORON_AMD_DECODE_PATH");
-    h->decode_path = dp && !strcmp(dp, "split") ? 1 : (dp && !strcmp(dp, "single") ? 2 : 0);
+    h->decode_path = !dp ? 0 : !strcmp(dp, "split") ? 1 : !strcmp(dp, "single") ? 2 : !strcmp(dp, "wave") ? 3 : 0;
 }
 
 /* General-parameter kernels: byte symbols (2 <= m <= 8) and 1 <= num_roots
@@ -1178,10 +1179,10 @@ static bool launch_split(poporon_t *h, const RsCorrParams &prm, const RsSplitWs 
         t.done();
     }
     {
-        /* what the split kernels hand on: one wave per codeword (rs_list1_k) */
+        /* what the split kernels hand on: one codeword per wave (rs_wave_k) */
         KernelTimer t(g, POPORON_AMD_KERNEL_LIST, s);
-        HIP_OK(rsk_list1(g.tab, &prm, d_data, ds, d_par, ps, count, ws.syn, ws.list, ws.nlist, ok, corrected,
-                         g.num_cu, s));
+        HIP_OK(rsk_wave(g.tab, &prm, d_data, ds, d_par, ps, count, ws.list, ws.nlist, ws.syn, nullptr, 0, nullptr,
+                        nullptr, 0, nullptr, ok, corrected, g.num_cu, s));
         t.done();
     }
     return true;
@@ -1219,6 +1220,16 @@ static bool launch_decode(poporon_t *h, uint8_t *d_data, size_t ds, uint8_t *d_p
         KernelTimer t(h->gpu, POPORON_AMD_KERNEL_SINGLE, s);
         HIP_OK(rsk_decode1(h->gpu.tab, &prm, ext_syn ? 2u : (pos8 || pos32) ? 1u : 0u, d_data, d_par, pos8, pos32,
                            cnt, 1u, ext_syn, ok, corrected, nullptr, 0, s));
+        t.done();
+        return true;
+    }
+    /* a few thousand codewords: one codeword per wave, syndromes included,
+     * one launch (the lane-per-codeword kernels would give each SIMD a few
+     * waves, each a ~10^4-step serial chain) */
+    if (h->decode_path == 3 || (h->decode_path == 0 && count < SPLIT_MIN_COUNT)) {
+        KernelTimer t(h->gpu, POPORON_AMD_KERNEL_WAVE, s);
+        HIP_OK(rsk_wave(h->gpu.tab, &prm, d_data, ds, d_par, ps, count, nullptr, nullptr, nullptr, ext_syn, ext_stride,
+                        pos8, pos32, pos_stride, cnt, ok, corrected, h->gpu.num_cu, s));
         t.done();
         return true;
     }
@@ -1289,9 +1300,11 @@ static bool launch_decode(poporon_t *h, uint8_t *d_data, size_t ds, uint8_t *d_p
                 }
             }
             {
+                /* what those hand on: one codeword per wave, in place (their
+                 * meta stays RS_ST_LIST: the block apply passes them by) */
                 KernelTimer t(g, POPORON_AMD_KERNEL_LIST, s);
-                HIP_OK(rsk_correct_era_list(g.tab, &prm, count, ws.syn, pos8, pos_stride, cnt, ok, corrected, ws.ext,
-                                            ws.meta, ws.list, ws.nlist, g.num_cu, s));
+                HIP_OK(rsk_wave(g.tab, &prm, d_data, ds, d_par, ps, count, ws.list, ws.nlist, ws.syn, nullptr, 0,
+                                pos8, nullptr, pos_stride, cnt, ok, corrected, g.num_cu, s));
                 t.done();
             }
         } else {

@@ -211,12 +211,17 @@ hipError_t rsk_serve(const RsDevTables *tab, const RsCorrParams *prm, uint8_t *z
 #define RS_SRV_DECODE 2u
 #define RS_SRV_STOP 3u   /* the server leaves (poporon_destroy) */
 
-/* the split error-mode decode's list, one wave per codeword (rs_single.hip
- * rs_list1_k): the codewords list[0 .. *list_n) decoded from their poly
- * syndromes and corrected in place; count bounds the grid */
-hipError_t rsk_list1(const RsDevTables *tab, const RsCorrParams *prm, uint8_t *data, size_t dstride, uint8_t *parity,
-                     size_t pstride, size_t count, const uint8_t *syn, const uint32_t *list, const uint32_t *list_n,
-                     uint8_t *ok, uint8_t *corrected, int num_cu, hipStream_t stream);
+/* rs_decode for one codeword per wave (rs_single.hip rs_wave_k), corrections
+ * in place, ok / corrected per codeword: codewords list[0 .. *list_n) when
+ * list != NULL (length read on the device), else 0 .. count - 1 (count bounds
+ * the grid either way).  Syndromes: syn (poly form, 32 B per codeword, the
+ * split decode's), syn16 (external log form), or neither: computed from the
+ * codeword.  pos8 / pos32 (at most one) with u8 counts: erasure mode. */
+hipError_t rsk_wave(const RsDevTables *tab, const RsCorrParams *prm, uint8_t *data, size_t dstride, uint8_t *parity,
+                    size_t pstride, size_t count, const uint32_t *list, const uint32_t *list_n, const uint8_t *syn,
+                    const uint16_t *syn16, size_t syn16_stride, const uint8_t *pos8, const uint32_t *pos32,
+                    size_t pos_stride, const uint8_t *cnt, uint8_t *ok, uint8_t *corrected, int num_cu,
+                    hipStream_t stream);
 
 /* poly syndromes (32 B per codeword, rsk_syndrome) -> log form: out[c*stride + i]
  * = log S_i (255 = zero), flag[c] = any S_i nonzero; out / flag may be NULL */

@@ -679,38 +679,53 @@ extern "C" hipError_t rsk_serve(const RsDevTables *tab, const RsCorrParams *prm,
 }
 
 /* ------------------------------------------------------------------------ */
-/* the split decode's list: one wave per codeword                            */
+/* one codeword per wave: small batches and the split decode's lists         */
 /* ------------------------------------------------------------------------ */
 
 /*
- * rs_list1_k: the error-mode codewords the split kernels hand on (L > 16, a
- * locator past x^16, deg != L: beyond capacity, the reference's failures and
- * miscorrections), decoded one codeword per WAVE with dec1_body's steps
- * (src/decode.c:49-227 with its integer semantics): Berlekamp-Massey with
- * coefficient i on lane i, Chien with four points per lane, Omega, Forney and
- * the re-syndrome check split over the two 32-lane halves, the corrections
- * applied in place.  A list is a few percent of a batch (~7 % of the
- * codewords of a binomial channel with mean 11.5 errors): one codeword per
- * lane put a few waves on each SIMD, each a ~10^4-step serial chain (0.24 ms
- * for 74k codewords of 2^20); one per wave puts the work of a codeword on 64
- * lanes and 32 waves on every CU.
+ * rs_wave_k: rs_decode (src/decode.c:431-487) for one codeword per WAVE with
+ * dec1_body's steps and integer semantics: syndromes (:375-415; each of the
+ * 32 over the two half-waves), or the split decode's poly syndromes, or
+ * external log-form syndromes (:446-464); erasure locator (:31-47) and
+ * Berlekamp-Massey (:49-96) with coefficient i on lane i; degree (:98-110);
+ * Chien (:112-145) with four points per lane; Omega (:147-158), Forney
+ * (:159-191) and the re-syndrome check (:193-209) over the two half-waves;
+ * the apply (:211-227) in place: error mode straight into the codeword
+ * (distinct locations), erasure mode through an LDS copy of the codeword
+ * (slot n gets root n's magnitude, repeated slots accumulate: quirks Q1-Q4).
  *
- * Four waves per workgroup share the GF tables; each wave loops over list
- * entries on its own (no workgroup barrier after the table fill).
+ * It serves what one codeword per lane serves badly: few codewords.  The
+ * lane-per-codeword kernels are a ~10^4-step serial chain per lane, so a
+ * batch of a few thousand codewords (a few waves per SIMD) or the split
+ * decode's list (the beyond-capacity codewords of a batch: 74k of 2^20 on a
+ * binomial channel with mean 11.5 errors took 0.36 ms there) costs the
+ * latency of that chain; here a codeword's work is spread over 64 lanes and
+ * 32 waves per CU run side by side.
+ *
+ * Four waves per workgroup share the GF tables (no workgroup barrier after
+ * their fill); each wave loops over its codewords: index e -> codeword
+ * list[e] (list mode, length read on the device) or e.
+ *
+ * Modes: syn == NULL && syn16 == NULL: syndromes from the codeword; syn: the
+ * split decode's poly syndromes (32 B per codeword); syn16: external log-form
+ * u16 syndromes (> 255 refused).  pos8 / pos32 (at most one): erasure mode,
+ * u8 counts in cnt.
  */
-#define L1_WG 256
+#define W_WG 256
 
-struct List1Wave {
+struct WaveState {
     uint32_t slog[64];  /* log S_i (ZL: zero), i < 32; ZL at 32..63 */
     uint32_t spoly[32];
     uint32_t llam[64];  /* log Lambda_j (ZL: zero), j <= 32; ZL past */
     uint32_t lom[32];
-    uint32_t roots[32], locs[32], mags[32];
+    uint32_t roots[32], locs[32], mags[32], pos[32];
+    uint16_t lw[256];   /* log of each codeword byte (ZL: zero or past the codeword) */
+    uint32_t cw[64];    /* the codeword (erasure-mode apply) */
 };
 
-struct List1Smem {
+struct WaveSmem {
     Tabs g;
-    List1Wave w[L1_WG / 64];
+    WaveState w[W_WG / 64];
 };
 
 /* lane order within a wave: LDS writes by some lanes, then reads by others */
@@ -729,91 +744,167 @@ __device__ __forceinline__ uint32_t other_half(uint32_t v, uint32_t lane)
     return lane < 32u ? a[1] : a[0];
 }
 
-__global__ __launch_bounds__(L1_WG) void rs_list1_k(const RsDevTables *__restrict__ T, RsCorrParams P, uint8_t *data,
-                                                    size_t dstride, uint8_t *parity, size_t pstride,
-                                                    const uint8_t *__restrict__ syn, const uint32_t *__restrict__ list,
-                                                    const uint32_t *__restrict__ list_n, uint8_t *__restrict__ okp,
-                                                    uint8_t *__restrict__ corp)
+template <typename PosT>
+__global__ __launch_bounds__(W_WG) void rs_wave_k(const RsDevTables *__restrict__ T, RsCorrParams P, uint8_t *data,
+                                                  size_t dstride, uint8_t *parity, size_t pstride, size_t count,
+                                                  const uint32_t *__restrict__ list, const uint32_t *__restrict__ list_n,
+                                                  const uint8_t *__restrict__ syn, const uint16_t *__restrict__ syn16,
+                                                  size_t syn16_stride, const PosT *__restrict__ pos, size_t pos_stride,
+                                                  const uint8_t *__restrict__ cnt, uint8_t *__restrict__ okp,
+                                                  uint8_t *__restrict__ corp)
 {
-    const uint32_t n = *list_n;
-    if ((size_t)blockIdx.x * (L1_WG / 64) >= n)
+    const size_t n = list ? (size_t)*list_n : count;
+    if ((size_t)blockIdx.x * (W_WG / 64) >= n)
         return;
-    __shared__ List1Smem sm;
+    __shared__ WaveSmem sm;
     const uint32_t t = threadIdx.x, lane = t & 63u, wave = t >> 6;
     fill_tabs(sm.g, T, t);
     __syncthreads();
     const Tabs &g = sm.g;
-    List1Wave &s = sm.w[wave];
+    WaveState &s = sm.w[wave];
     const uint32_t size = P.size, L = size + RS_NR;
     const int32_t pad = P.pad;
     const bool co = lane <= RS_NR;
-    for (uint32_t e = blockIdx.x * (L1_WG / 64) + wave; e < n; e += gridDim.x * (L1_WG / 64)) {
-        const size_t cw = list[e];
-        /* ---- syndromes (poly form, rsk_syndrome) -> log form ---- */
-        const uint32_t v = lane < RS_NR ? syn[cw * RS_NR + lane] : 0u;
-        if (lane < RS_NR)
-            s.spoly[lane] = v;
-        s.slog[lane] = lane < RS_NR ? (uint32_t)g.lg[v] : ZL;
-        wave_sync();
-
-        /* ---- Berlekamp-Massey, error mode (r = 1..32): dec1_body's loop
-         * with no erasures ---- */
-        uint32_t lam = lane == 0 ? 1u : 0u;
-        uint32_t llam = g.lg[lam];
-        uint32_t B = llam, Lr = 0;
-        uint32_t term = g.ex[llam + s.slog[lane == 0 ? 0u : 63u]];
-        uint32_t s1 = s.slog[lane <= 1u ? 1u - lane : 63u];
-        for (uint32_t r = 1u; r <= RS_NR; ++r) {
-            const uint32_t disc = wave_xor_v(term);
-            const uint32_t bs = wave_up_old(B, ZL);
-            const uint32_t ld = g.lg[disc];
-            const uint32_t dq = red(ld + bs);
-            const uint32_t t1 = g.ex[llam + s1], t2 = g.ex[dq + s1], up = g.ex[dq];
-            s1 = s.slog[lane <= r + 1u && r + 1u < RS_NR ? r + 1u - lane : 63u];
-            term = t1 ^ t2;
-            const uint32_t ds = __builtin_amdgcn_readfirstlane(disc);
-            const bool len = ds != 0u && 2u * Lr <= r - 1u; /* uniform */
-            const uint32_t bl = lam ? red(llam + 255u - ld) : ZL;
-            B = len ? bl : bs;
-            Lr = len ? r - Lr : Lr;
-            lam ^= up;
-            llam = g.lg[lam];
+    const bool era = pos != nullptr;
+    for (size_t e = (size_t)blockIdx.x * (W_WG / 64) + wave; e < n; e += (size_t)gridDim.x * (W_WG / 64)) {
+        const size_t c = list ? (size_t)list[e] : e;
+        uint8_t *cdata = data + c * dstride, *cpar = parity + c * pstride;
+        /* ---- inputs: the codeword where the syndromes or the erasure apply
+         * need it (lane j, j + 64, ...: coalesced), the slots ---- */
+        uint32_t w4[4] = {0, 0, 0, 0};
+        const bool own_syn = syn == nullptr && syn16 == nullptr;
+        if (own_syn || era) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const uint32_t j = lane + 64u * k;
+                w4[k] = j < size ? cdata[j] : j < L ? cpar[j - size] : 0u;
+            }
         }
-        const uint64_t nz = __ballot(co && lam != 0u);
-        const uint32_t deg = 63u - (uint32_t)__builtin_clzll(nz); /* lane 0 holds Lambda_0 = 1 */
-        s.llam[lane] = co ? llam : ZL;
+        uint32_t ne = 0;
+        if (era) {
+            ne = cnt[c];
+            if (lane < RS_NR)
+                s.pos[lane] = (uint32_t)pos[c * pos_stride + lane];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const uint32_t j = lane + 64u * k;
+                reinterpret_cast<uint8_t *>(s.cw)[j] = (uint8_t)w4[k];
+            }
+        }
+        /* ---- syndromes, log form ---- */
+        bool refuse = false;
+        uint32_t sv = 0; /* S_i as a field element, lanes < 32 */
+        if (own_syn) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                s.lw[lane + 64u * k] = (uint16_t)g.lg[w4[k]]; /* ZL past the codeword (w = 0) */
+            wave_sync();
+            /* S_i = sum_j w_j beta_i^(L-1-j), beta_i = alpha^(prim (fcr+i)) (the
+             * reference's Horner steps, exact for these parameters): lane l
+             * sums syndrome i = l & 31 over j = (l >> 5) + 2k */
+            const uint32_t i = lane & 31u, g0 = lane >> 5;
+            const uint32_t b = m255(P.prim * (P.fcr + i));
+            const uint32_t d2 = m255(2u * b);
+            uint32_t ex = m255(b * (L - 1u - g0)), acc = 0;
+#pragma unroll 8
+            for (uint32_t k = 0; k < 128u; ++k) {
+                acc ^= g.ex[s.lw[g0 + 2u * k] + ex]; /* j <= 255: ZL past the codeword */
+                ex = ex >= d2 ? ex - d2 : ex + 255u - d2;
+            }
+            sv = acc ^ other_half(acc, lane);
+        } else if (syn) {
+            sv = lane < RS_NR ? syn[c * RS_NR + lane] : 0u;
+        }
+        if (syn16) {
+            const uint32_t xs = lane < RS_NR ? syn16[c * syn16_stride + lane] : 255u;
+            refuse = __ballot(xs > 255u) != 0ull; /* out-of-table in the reference: refused */
+            if (lane < RS_NR) {
+                s.slog[lane] = xs >= 255u ? ZL : xs;
+                s.spoly[lane] = xs >= 255u ? 0u : g.ex[xs];
+            } else {
+                s.slog[lane] = ZL;
+            }
+        } else {
+            if (lane < RS_NR)
+                s.spoly[lane] = sv;
+            s.slog[lane] = lane < RS_NR ? (uint32_t)g.lg[sv] : ZL;
+        }
+        const bool any = __ballot(lane < RS_NR && s.slog[lane] != ZL) != 0ull;
         wave_sync();
         uint32_t ok = 0, fixed = 0;
-        bool fail = deg == 0u; /* src/decode.c:108-110 */
+        /* a clean codeword succeeds whatever its erasure count (src/decode.c:468);
+         * a dirty one with more erasures than roots overflows the reference's
+         * locator (quirk Q5): refused, as every other kernel */
+        bool fail = refuse || !any || (era && ne > RS_NR);
+        if (!refuse && !any)
+            ok = 1;
+
+        uint32_t deg = 0;
+        if (!fail) {
+            /* ---- erasure locator and Berlekamp-Massey (dec1_body's wave-0
+             * loop): lane i holds Lambda_i (poly and log) and B_i (log) ---- */
+            uint32_t lam = lane == 0 ? 1u : 0u;
+            for (uint32_t l = 0; l < ne; ++l) {
+                const uint32_t xl =
+                    ((P.prim * (uint32_t)(RS_NN - 1u - (s.pos[l] + (uint32_t)pad))) & 0xffffu) % 255u;
+                const uint32_t prev = wave_up(lam, lane, 0u);
+                lam ^= lane ? g.ex[xl + g.lg[prev]] : 0u;
+            }
+            uint32_t llam = g.lg[lam];
+            uint32_t B = llam, Lr = ne;
+            uint32_t term = g.ex[llam + s.slog[lane <= ne ? ne - lane : 63u]];
+            uint32_t s1 = s.slog[lane <= ne + 1u && ne + 1u < RS_NR ? ne + 1u - lane : 63u];
+            for (uint32_t r = ne + 1u; r <= RS_NR; ++r) {
+                const uint32_t disc = wave_xor_v(term);
+                const uint32_t bs = wave_up_old(B, ZL);
+                const uint32_t ld = g.lg[disc];
+                const uint32_t dq = red(ld + bs);
+                const uint32_t t1 = g.ex[llam + s1], t2 = g.ex[dq + s1], up = g.ex[dq];
+                s1 = s.slog[lane <= r + 1u && r + 1u < RS_NR ? r + 1u - lane : 63u];
+                term = t1 ^ t2;
+                const uint32_t ds = __builtin_amdgcn_readfirstlane(disc);
+                const bool len = ds != 0u && 2u * Lr <= r + ne - 1u; /* uniform */
+                const uint32_t bl = lam ? red(llam + 255u - ld) : ZL;
+                B = len ? bl : bs;
+                Lr = len ? r + ne - Lr : Lr;
+                lam ^= up;
+                llam = g.lg[lam];
+            }
+            const uint64_t nz = __ballot(co && lam != 0u);
+            deg = 63u - (uint32_t)__builtin_clzll(nz); /* lane 0 holds Lambda_0 = 1 */
+            s.llam[lane] = co ? llam : ZL;
+            wave_sync();
+            fail = deg == 0u; /* src/decode.c:108-110 */
+        }
 
         /* ---- Chien, src/decode.c:117-145: points i = 64 k + lane + 1 ---- */
-        uint32_t total = 0;
         if (!fail) {
+            uint32_t total = 0;
 #pragma unroll 1
             for (uint32_t k = 0; k < 4; ++k) {
                 const uint32_t i = 64u * k + lane + 1u, ii = i == 255u ? 0u : i;
-                uint32_t ev = 1u, ex = 0;
+                uint32_t ev = 1u, ee = 0;
 #pragma unroll 8
                 for (uint32_t j = 1; j <= deg; ++j) {
-                    ex = red(ex + ii);
-                    ev ^= g.ex[s.llam[j] + ex];
+                    ee = red(ee + ii);
+                    ev ^= g.ex[s.llam[j] + ee];
                 }
                 const bool root = i <= 255u && ev == 0u;
                 const uint64_t rb = __ballot(root);
+                const uint32_t loc = (i * P.iprim + 254u) % 255u;
                 if (root) {
                     const uint32_t idx = total + (uint32_t)__builtin_popcountll(rb & ((1ull << lane) - 1ull));
-                    const uint32_t loc = (i * P.iprim + 254u) % 255u;
                     if (idx < RS_NR) {
                         s.roots[idx] = i;
                         s.locs[idx] = loc;
                     }
                 }
-                fail |= __ballot(root && (int32_t)((i * P.iprim + 254u) % 255u) < pad) != 0ull; /* :132-134 */
+                fail |= __ballot(root && (int32_t)loc < pad) != 0ull; /* :132-134 */
                 total += (uint32_t)__builtin_popcountll(rb);
             }
             fail |= total != deg; /* src/decode.c:143-145 */
+            wave_sync();
         }
-        wave_sync();
 
         if (!fail) {
             /* ---- Omega_m = sum_(j <= m) S_(m-j) Lambda_j, m < deg: lane m
@@ -874,38 +965,73 @@ __global__ __launch_bounds__(L1_WG) void rs_list1_k(const RsDevTables *__restric
             chk ^= other_half(chk, lane);
             fail |= __ballot(lane < 32u && chk != s.spoly[i]) != 0ull;
 
-            /* ---- apply, src/decode.c:215-226 (error mode): locations from
-             * Chien lie in [pad, 254], so none is out of range ---- */
+            /* ---- apply, src/decode.c:211-227 ---- */
             if (!fail) {
                 ok = 1;
-                if (lane < deg) {
-                    const uint32_t p = (uint32_t)((int32_t)s.locs[lane] - pad);
-                    if (mag && p < L) {
-                        uint8_t *d = p < size ? data + cw * dstride + p : parity + cw * pstride + (p - size);
-                        *d = (uint8_t)(*d ^ mag);
+                if (!era) { /* error mode: Chien locations lie in [pad, 254]: none out of range */
+                    if (lane < deg) {
+                        const uint32_t p = (uint32_t)((int32_t)s.locs[lane] - pad);
+                        if (mag && p < L) {
+                            uint8_t *d = p < size ? cdata + p : cpar + (p - size);
+                            *d = (uint8_t)(*d ^ mag);
+                        }
+                    }
+                } else {
+                    /* erasure mode: magnitude q (ascending location) into slot q
+                     * (Q1/Q2); slots past the codeword: parity when < size + 32
+                     * (Q4), else dropped; repeated slots accumulate */
+                    if (lane < deg) {
+                        const uint32_t p = s.pos[lane];
+                        if (mag && p < L)
+                            atomicXor(&s.cw[p >> 2], mag << (8u * (p & 3u)));
+                    }
+                    wave_sync();
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) {
+                        const uint32_t j = lane + 64u * k;
+                        const uint32_t v = reinterpret_cast<const uint8_t *>(s.cw)[j];
+                        if (j < L && v != w4[k]) {
+                            if (j < size)
+                                cdata[j] = (uint8_t)v;
+                            else
+                                cpar[j - size] = (uint8_t)v;
+                        }
                     }
                 }
             }
         }
         if (lane == 0) {
-            okp[cw] = (uint8_t)ok;
+            okp[c] = (uint8_t)ok;
             if (corp)
-                corp[cw] = (uint8_t)fixed;
+                corp[c] = (uint8_t)fixed;
         }
         wave_sync(); /* this codeword's LDS reads before the next one's writes */
     }
 }
 
-extern "C" hipError_t rsk_list1(const RsDevTables *tab, const RsCorrParams *prm, uint8_t *data, size_t dstride,
-                                uint8_t *parity, size_t pstride, size_t count, const uint8_t *syn, const uint32_t *list,
-                                const uint32_t *list_n, uint8_t *ok, uint8_t *corrected, int num_cu, hipStream_t stream)
+/* the grid: eight 4-wave workgroups per CU (32 waves), fewer for a small
+ * batch; workgroups past a list's length (read on the device) leave at once */
+static dim3 wave_grid(size_t count, int num_cu)
+{
+    const size_t cap = 8u * (size_t)(num_cu > 0 ? num_cu : 256), need = (count + 3) / 4;
+    return dim3((uint32_t)(need < cap ? (need ? need : 1) : cap));
+}
+
+extern "C" hipError_t rsk_wave(const RsDevTables *tab, const RsCorrParams *prm, uint8_t *data, size_t dstride,
+                               uint8_t *parity, size_t pstride, size_t count, const uint32_t *list,
+                               const uint32_t *list_n, const uint8_t *syn, const uint16_t *syn16,
+                               size_t syn16_stride, const uint8_t *pos8, const uint32_t *pos32, size_t pos_stride,
+                               const uint8_t *cnt, uint8_t *ok, uint8_t *corrected, int num_cu, hipStream_t stream)
 {
     if (count == 0)
         return hipSuccess;
-    /* eight 4-wave workgroups per CU (32 waves), fewer for a small batch;
-     * workgroups past the list's length (read on the device) leave at once */
-    const size_t cap = 8u * (size_t)(num_cu > 0 ? num_cu : 256), need = (count + 3) / 4;
-    RS_LAUNCH(rs_list1_k, dim3((uint32_t)(need < cap ? need : cap)), dim3(L1_WG), 0, stream, tab, *prm, data, dstride,
-              parity, pstride, syn, list, list_n, ok, corrected);
+    if (pos32)
+        RS_LAUNCH(rs_wave_k<uint32_t>, wave_grid(count, num_cu), dim3(W_WG), 0, stream, tab, *prm, data, dstride,
+                  parity, pstride, count, list, list_n, syn, syn16, syn16_stride, pos32, pos_stride, cnt, ok,
+                  corrected);
+    else
+        RS_LAUNCH(rs_wave_k<uint8_t>, wave_grid(count, num_cu), dim3(W_WG), 0, stream, tab, *prm, data, dstride,
+                  parity, pstride, count, list, list_n, syn, syn16, syn16_stride, pos8, pos_stride, cnt, ok,
+                  corrected);
     return hipGetLastError();
 }

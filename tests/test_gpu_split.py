@@ -15,7 +15,7 @@ import libpoporon_amd as P
 pytestmark = pytest.mark.gpu
 
 NR = 32
-PATHS = ["split", "single"]
+PATHS = ["split", "single", "wave"]
 
 
 def _handle(monkeypatch, path, params=(8, 0x11D, 1, 1, 32)):
