@@ -549,7 +549,8 @@ finish:
     /* STAMP 8 */
     if (t == 0) {
         *okp = (uint8_t)ok;
-        *corp = (uint8_t)fixed;
+        if (corp) /* the batch API's d_corrected may be NULL */
+            *corp = (uint8_t)fixed;
     }
 }
 

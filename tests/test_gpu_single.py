@@ -169,6 +169,29 @@ def test_batch_of_one_device(oracle_default):
     assert t[P.KERNEL_SINGLE][1] == 1 and t[P.KERNEL_CORRECT][1] == 0 and t[P.KERNEL_REMAINDER][1] == 0
 
 
+@pytest.mark.parametrize("n", [1, 2, 300, 8192])
+def test_batch_device_without_corrected(oracle_default, n):
+    """poporon_decode_batch_device with d_corrected NULL (optional in the
+    header) on each batch route: rs_dec1_k (1), rs_wave_k (2, 300) and the
+    split kernels (8192)."""
+    _need_gpu()
+    import torch
+    h = P.Poporon.default()
+    rng = np.random.default_rng(n)
+    data = rng.integers(0, 256, (n, 223), dtype=np.uint8)
+    cw = np.concatenate([data, oracle_default.encode_batch(data)], 1)
+    for i in range(n):
+        cw[i, rng.permutation(255)[:16]] ^= rng.integers(1, 256, 16, dtype=np.uint8)
+    want = oracle_default.decode_batch(cw[:, :223], cw[:, 223:])
+    d = torch.from_numpy(cw).cuda()
+    ok = torch.zeros(n, dtype=torch.uint8, device="cuda")
+    b = d.data_ptr()
+    h.decode_batch_device(b, 255, b + 223, 255, 223, n, ok.data_ptr(), None)
+    torch.cuda.synchronize()
+    assert (ok.cpu().numpy() == np.asarray(want[0]).astype(np.uint8)).all()
+    assert (d.cpu().numpy()[:, :223] == np.asarray(want[2])).all()
+
+
 def test_single_call_many(oracle_default):
     """2000 back-to-back poporon_encode / poporon_decode calls (the latency
     path: completion words polled in host memory), 16 errors each."""
