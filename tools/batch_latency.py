@@ -5,7 +5,7 @@ reps, stream-synchronised), for n from 1 to 2^20.
 
     python tools/batch_latency.py [--reps 20]
 
-POPORON_AMD_DECODE_PATH=split|single selects the decode route as in the
+POPORON_AMD_DECODE_PATH=split|single|wave selects the decode route as in the
 tests (default: split from 8,192 codewords on)."""
 import argparse
 import json
@@ -32,7 +32,7 @@ def main():
     K, N = 223, 255
     s = torch.cuda.current_stream().cuda_stream
     out = {"path": os.environ.get("POPORON_AMD_DECODE_PATH", "default"), "us": {}}
-    for n in (1, 16, 256, 1024, 4096, 8191, 8192, 65536, 1 << 20):
+    for n in (1, 16, 256, 1024, 4096, 8191, 8192, 12288, 16384, 24576, 32768, 65536, 1 << 20):
         cw = torch.zeros((n, N), dtype=torch.uint8, device=dev)
         cw[:, :K] = devdata.synth_bytes(bench.SEED, 0, n, K, dev)
         b = cw.data_ptr()

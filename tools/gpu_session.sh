@@ -29,7 +29,8 @@ for step in "$@"; do
     lat) run lat 200 python tools/lat_single.py 2000
          POPORON_AMD_SERVE=0 run lat_noserve 200 python tools/lat_single.py 2000 ;;
     batchlat) run batchlat 300 python tools/batch_latency.py
-              POPORON_AMD_DECODE_PATH=split run batchlat_split 300 python tools/batch_latency.py ;;
+              POPORON_AMD_DECODE_PATH=split run batchlat_split 300 python tools/batch_latency.py
+              POPORON_AMD_DECODE_PATH=wave run batchlat_wave 300 python tools/batch_latency.py ;;
     ab) # A/B of the experiment builds in build/*.so, alternated twice (same box)
         run ab 900 python tools/exp_bench.py $(ls build/*.so) $(ls build/*.so) ;;
     prof) run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- \

@@ -39,7 +39,7 @@ PATTERNS = [
     (r"\brs_bm_k\b|\brs_ebm_k\b", bench.K_BM), (r"\brs_chien_k\b|\brs_chien32_k\b", bench.K_CHIEN),
     (r"rs_forney_k|rs_forney32_k", bench.K_FORNEY),
     (r"rs_apply_k", bench.K_APPLY), (r"\brs_era_bp_k\b|\brs_era_k\b", bench.K_ERASURE),
-    (r"\brs_list1_k\b|rs_correct_k<[^>]*true>|rs_correct_list|rs_correct_k", bench.K_LIST),
+    (r"\brs_wave_k\b|\brs_list1_k\b|rs_correct_k<[^>]*true>|rs_correct_list|rs_correct_k", bench.K_LIST),
 ]
 
 
