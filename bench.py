@@ -22,13 +22,15 @@ configs[4] (strong split): --c4-total codewords (default 2^26) are split into
 contiguous ranges over the ranks (libpoporon_amd's own partition); each rank
 encodes, corrupts (untimed) and decodes its range; the line reports their
 cw/s (max-over-ranks time) and a checksum of every decoded codeword that is
-identical for every GPU count.
+identical for every GPU count.  --c4-scatter T (opt-in, N > 1) adds the split
+as a data movement: rank 0 holds T corrupted codewords and sends each rank its
+range point-to-point (RCCL send/recv over xGMI) before every rank decodes it.
 
 Multi-GPU: `bench.py --gpus N` starts N ranks itself (torch.distributed.run as
 a child process, before anything touches the GPU) unless it already runs
 under a launcher (WORLD_SIZE set, which must equal N).  One process per GPU,
 RCCL (`nccl` backend) only for barriers and the max-time / checksum
-reductions; no data-path collective.
+reductions; no data-path collective (but for the opt-in --c4-scatter).
 
 Also reported: per-kernel HIP-event times (in-library, stamped by each kernel's dispatch),
 the roofline of the dominant kernel, erasure decode (configs[3]), the
@@ -75,6 +77,10 @@ def parse_args(argv=None):
     ap.add_argument("--c4-chunk", type=int, default=1 << 24, help="configs[4]: codewords per rank-chunk (memory)")
     ap.add_argument("--c4-reps", type=int, default=2)
     ap.add_argument("--no-c4", action="store_true")
+    ap.add_argument("--c4-scatter", type=int, default=0,
+                    help="configs[4] as a data movement (N > 1, opt-in): rank 0 holds this many corrupted codewords "
+                         "and sends each rank its range point-to-point (RCCL send/recv over xGMI), then every rank "
+                         "decodes its range")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-erasure", action="store_true")
     ap.add_argument("--no-mixed", action="store_true", help="skip the mixed-channel decode (binomial error counts)")
@@ -202,6 +208,22 @@ class Ranks:
         import torch
         import torch.distributed as dist
         self.world, self.device, self.torch, self.dist = world, device, torch, dist
+        self.rank = dist.get_rank() if world > 1 else 0
+
+    def scatter_rows(self, out, chunks):
+        """Rank 0 sends chunks[r] to rank r point-to-point (RCCL send/recv:
+        over xGMI between GPUs; gloo on CPU tests) and copies chunks[0]
+        into its own `out`; every other rank receives into `out`."""
+        torch, dist = self.torch, self.dist
+        t = lambda a: a if isinstance(a, torch.Tensor) else torch.from_numpy(a)  # noqa: E731
+        if self.rank == 0:
+            ops = [dist.P2POp(dist.isend, t(chunks[r]), r) for r in range(1, self.world)]
+            t(out).copy_(t(chunks[0]))
+        else:
+            ops = [dist.P2POp(dist.irecv, t(out), 0)]
+        if ops:
+            for req in dist.batch_isend_irecv(ops):
+                req.wait()
 
     def barrier(self, sync):
         sync()
@@ -406,6 +428,54 @@ def run_strong(be, ranks, args, rank, world):
             "parity_checksum": cs_out,
             "_samples": {"configs4_encode": {k: np.concatenate(v) for k, v in senc.items()},
                          "configs4_decode16": {k: np.concatenate(v) for k, v in sdec.items()}}}
+
+
+def run_scatter(be, ranks, args, rank, world):
+    """configs[4]'s "batch split" with the data movement in it (opt-in,
+    --c4-scatter T): rank 0 holds T encoded and corrupted codewords (16
+    errors each) and sends rank r its range [T*r/N, T*(r+1)/N) point-to-point
+    (RCCL send/recv: the xGMI links from GPU 0), then every rank decodes its
+    range.  Timed: scatter, and scatter + decode, max over ranks (best of
+    --c4-reps; the first exchange sets up the P2P channels).  Verified: every
+    codeword decoded with ok = 1, corrected = 16, and the checksum of all
+    decoded codewords equal to that of the encoded batch."""
+    total = args.c4_scatter
+    lo, hi = shard(total, rank, world)
+    mine = be.rows(hi - lo)
+    chunks, csum_clean = None, 0
+    if rank == 0:
+        src = be.rows(total)
+        be.synth_messages(src, 0, seed=SEED + 11)
+        be.encode(src)
+        csum_clean = be.checksum(src, 0)
+        err = be.errors(0, total, 16, N, SEED + 12)
+        be.channel(src, err)
+        del err
+        chunks = [src[shard(total, r, world)[0]:shard(total, r, world)[1]] for r in range(world)]
+    st = be.status(hi - lo)
+    t_sc, t_all = None, None
+    for _ in range(max(2, args.c4_reps)):
+        ranks.barrier(be.sync)
+        t0 = time.perf_counter()
+        ranks.scatter_rows(mine, chunks)
+        be.sync()
+        t1 = time.perf_counter()
+        be.decode(mine, st)
+        be.sync()
+        t2 = time.perf_counter()
+        a, b = ranks.max(t1 - t0), ranks.max(t2 - t0)
+        t_sc, t_all = (a, b) if t_sc is None else (min(t_sc, a), min(t_all, b))
+    nbad = ranks.sum_int(be.n_bad(st, 16))
+    cs_out = ranks.sum_u64(be.checksum(mine, lo))
+    cs_in = ranks.sum_u64(csum_clean)
+    moved = (total - shard(total, 0, world)[1]) * N  # bytes that leave rank 0
+    return {"total_codewords": total, "n_gpus": world, "split": "contiguous ranges [T*r/N, T*(r+1)/N) from rank 0",
+            "scatter_ms": round(t_sc * 1e3, 3), "scatter_GB_per_s": round(moved / t_sc / 1e9, 2) if t_sc > 0 else None,
+            "scatter_decode_ms": round(t_all * 1e3, 3),
+            "cw_per_s": round(total / t_all, 1) if t_all > 0 else None,
+            "timed": "send/recv of the ranges + decode@16 of each range, max over ranks; synthesis, encode and "
+                     "channel on rank 0 untimed",
+            "verified": nbad == 0 and cs_in == cs_out, "parity_checksum": cs_out}
 
 
 # ----------------------------------------------------------------------------
@@ -1095,6 +1165,10 @@ def main(argv=None):
         line["configs4"] = c4
         line["parity_checksum"] = c4["parity_checksum"]
         line["verified"] = line["verified"] and c4["verified"]
+    if args.c4_scatter and world > 1:
+        sc = run_scatter(be, ranks, args, rank, world)
+        line["configs4_scatter"] = sc
+        line["verified"] = line["verified"] and sc["verified"]
     # every sampled codeword of every mode against the reference CPU path
     # (after all timed loops)
     ps = parity_sample(samples, ranks)

@@ -99,3 +99,19 @@ def test_error_patterns_unique_and_in_range():
     up, um = T.synth_errors_cpu(bench.SEED + 2, 0, 256, 32, 223)
     for r in range(256):
         assert dict(zip(up[r].tolist(), um[r].tolist())) == dict(zip(epos[r].tolist(), emag[r].tolist()))
+
+
+def test_scatter_from_rank0():
+    """--c4-scatter: rank 0 sends each rank its range point-to-point (gloo
+    here, RCCL send/recv on GPUs); every codeword decodes, and the checksum
+    equals the encoded batch's, computed independently here."""
+    r = _line(_run(2, ("--no-c4", "--c4-scatter", "600", "--c4-reps", "1")))
+    sc = r["configs4_scatter"]
+    assert r["verified"] and sc["verified"] and sc["n_gpus"] == 2 and sc["total_codewords"] == 600
+    assert sc["scatter_ms"] > 0 and sc["scatter_decode_ms"] >= sc["scatter_ms"]
+    from oracle import Oracle
+    msgs = T.synth_rows_cpu(bench.SEED + 11, 0, 600, 223)
+    cw = np.concatenate([msgs, Oracle().encode_batch(msgs)], 1)
+    assert T.checksum_cpu(cw, 0) == sc["parity_checksum"]
+    one = _line(_run(1, ("--no-c4", "--c4-scatter", "600")))
+    assert "configs4_scatter" not in one  # nothing to move on one rank

@@ -28,6 +28,8 @@ for step in "$@"; do
     bench) run bench 600 python bench.py ;;
     lat) run lat 200 python tools/lat_single.py 2000
          POPORON_AMD_SERVE=0 run lat_noserve 200 python tools/lat_single.py 2000 ;;
+    bsz) run bsz 700 bash tools/batch_sizes.sh ;;
+    batchwave) POPORON_AMD_DECODE_PATH=wave run batchlat_wave 300 python tools/batch_latency.py ;;
     batchlat) run batchlat 300 python tools/batch_latency.py
               POPORON_AMD_DECODE_PATH=split run batchlat_split 300 python tools/batch_latency.py
               POPORON_AMD_DECODE_PATH=wave run batchlat_wave 300 python tools/batch_latency.py ;;
