@@ -140,10 +140,10 @@ bool poporon_decode_batch(poporon_t *pprn, uint8_t *data, size_t data_stride, ui
  * batches of that size: 1, 9 = the 32-sorted-erasure kernel (prim 1), 4 / 5
  * / 6 = the errata kernels, 7 = the same per-wave decoder over the rest, 8 =
  * apply.  A batch of one codeword: 10 = the one-workgroup decoder
- * (rs_dec1_k), 0 = encode (rs_enc1_k).  Batches of 2..8191 codewords: 11 =
+ * (rs_dec1_k), 0 = encode (rs_enc1_k).  Batches of 2..16383 codewords: 11 =
  * the one-codeword-per-wave decoder (rs_wave_k, syndromes included).
  *
- * Error- and erasure-mode batches of at least 8192 codewords take the split
+ * Error- and erasure-mode batches of at least 16384 codewords take the split
  * decode; POPORON_AMD_DECODE_PATH=split / single / wave in the environment
  * at poporon_create forces the split kernels, the lane-per-codeword general
  * kernel (rs_correct_k) or the per-wave decoder for every batch size. */

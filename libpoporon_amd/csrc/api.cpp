@@ -1142,9 +1142,12 @@ static bool launch_encode(poporon_t *h, const uint8_t *d_data, size_t ds, uint8_
     return true;
 }
 
-/* error-mode batches from this size on take the split kernels (rs_fast.hip:
- * five launches instead of two, each at twice the occupancy) */
-#define SPLIT_MIN_COUNT 8192
+/* batches from this size on take the split kernels (rs_fast.hip, six
+ * launches, one codeword per lane); smaller ones one launch of rs_wave_k (one
+ * codeword per wave).  Where they cross (16 errors, wall time per call,
+ * profiles/r04_batchlat_*.log): 12,288 codewords 86 vs ~108 us, 16,384 107 vs
+ * ~108, 32,768 196 vs ~110 */
+#define SPLIT_MIN_COUNT 16384
 
 /* the split error-mode decode of one sub-batch (rs_fast.hip) */
 static bool launch_split(poporon_t *h, const RsCorrParams &prm, const RsSplitWs &ws, uint8_t *d_data, size_t ds,

@@ -169,11 +169,11 @@ def test_batch_of_one_device(oracle_default):
     assert t[P.KERNEL_SINGLE][1] == 1 and t[P.KERNEL_CORRECT][1] == 0 and t[P.KERNEL_REMAINDER][1] == 0
 
 
-@pytest.mark.parametrize("n", [1, 2, 300, 8192])
+@pytest.mark.parametrize("n", [1, 2, 300, 16384])
 def test_batch_device_without_corrected(oracle_default, n):
     """poporon_decode_batch_device with d_corrected NULL (optional in the
     header) on each batch route: rs_dec1_k (1), rs_wave_k (2, 300) and the
-    split kernels (8192)."""
+    split kernels (16384)."""
     _need_gpu()
     import torch
     h = P.Poporon.default()
