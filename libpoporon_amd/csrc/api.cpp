@@ -476,15 +476,8 @@ static void build_tables(poporon_t *h)
     p.prim = rs->primitive_element;
     p.iprim = h->primitive_inverse;
     p.vfast = ((uint64_t)(p.fcr + RS_NR - 1) * p.prim * 254u) < 32768u;
-    /* the LFSR computes c(x) x^32 mod g, so S_i = r(beta_i) beta_i^-32 =
-     * sum_m r_m beta_i^-(m+1), beta_i = alpha^(prim (fcr + i)) */
-    for (uint32_t m = 0; m < RS_NR; m++) {
-        const long long a = (long long)(m + 1) * p.prim;
-        p.tr_inc[m] = (uint8_t)((255 - (a % 255)) % 255);
-        p.tr_start[m] = (uint8_t)((255 - ((a * p.fcr) % 255)) % 255);
-    }
 
-    /* remainder -> syndrome nibble tables (rs_device.h) */
+    /* E' -> syndrome nibble tables (rs_device.h) */
     auto gmul = [&](uint32_t x, uint32_t logc) -> uint8_t {
         return x == 0 ? 0 : (uint8_t)gf->log2exp[(gf->exp2log[x] + logc) % 255];
     };
@@ -493,8 +486,8 @@ static void build_tables(poporon_t *h)
             for (uint32_t v = 0; v < 16; v++) {
                 uint8_t rowb[RS_NR];
                 for (uint32_t i = 0; i < RS_NR; i++) {
-                    const uint64_t e = (uint64_t)(m + 1) * p.prim * (p.fcr + i);
-                    rowb[i] = gmul(v << (4 * n), (uint32_t)((255 - (e % 255)) % 255));
+                    const uint64_t e = (uint64_t)(RS_NR - 1 - m) * p.prim * (p.fcr + i);
+                    rowb[i] = gmul(v << (4 * n), (uint32_t)(e % 255));
                 }
                 memcpy(&t.synt[((m * 2 + n) * 2 + 0) * 16 + v], rowb, 16);
                 memcpy(&t.synt[((m * 2 + n) * 2 + 1) * 16 + v], rowb + 16, 16);

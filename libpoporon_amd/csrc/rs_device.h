@@ -53,11 +53,14 @@ struct RsDevTables {
     uint4 lfsr[512];
     uint8_t exp2[512];
     uint8_t log[256];
-    /* synt: remainder -> syndromes, nibble tables.  For remainder byte m,
-     * nibble half n (0 = low, 1 = high) and nibble value v, the 32-byte row
-     * (S_i contribution, i = 0..31) is split in two 16-byte planes h:
+    /* synt: E' -> syndromes, nibble tables.  E' = the received parity +
+     * the parity of the received data (32 bytes, byte m = coefficient of
+     * x^(31-m)): the received word is a codeword + E'(x), so S_i = E'(beta_i).
+     * For byte m, nibble half n (0 = low, 1 = high) and nibble value v, the
+     * 32-byte row (S_i contribution, i = 0..31) is split in two 16-byte
+     * planes h:
      *   synt[((m*2 + n)*2 + h)*16 + v]  = bytes i = 16h .. 16h+15 of
-     *   (v << 4n) * beta_i^-(m+1)   (see RsCorrParams for beta_i).
+     *   (v << 4n) * beta_i^(31-m)   (see RsCorrParams for beta_i).
      * Plane-major layout keeps the 16 rows of a plane in 16 distinct LDS
      * bank slots. */
     uint4 synt[32 * 2 * 2 * 16];
@@ -83,20 +86,14 @@ struct RsDevTables {
 };
 #define RS_Z0 200u /* zero sentinel row of gfa (rs_fast.hip) */
 
-/*
- * Parameters of the correction kernel (by value).  tr_start/tr_inc turn the
- * 32-byte remainder r (byte m = coefficient of x^(31-m)) into the syndromes
- * S_i = r(beta_i), beta_i = alpha^(prim*(fcr+i)):
- *   log(r_m * beta_i^(31-m)) = log r_m + tr_start[m] + i*tr_inc[m]  (mod 255).
- */
+/* Parameters of the decode kernels (by value); the syndromes are
+ * S_i = c(beta_i), beta_i = alpha^(prim*(fcr+i)). */
 struct RsCorrParams {
     uint32_t fcr, prim, iprim;
     uint32_t size;   /* message bytes per codeword (1..223) */
     int32_t pad;     /* 255 - 32 - size */
     uint32_t vfast;  /* (fcr+31)*prim*254 < 32768: verification exponents need no int16 emulation */
     uint32_t force_verify; /* run the re-syndrome check even where it provably passes (tests) */
-    uint8_t tr_start[RS_NR];
-    uint8_t tr_inc[RS_NR];
 };
 
 /*
@@ -156,8 +153,9 @@ extern "C" {
 hipError_t rsk_encode(const RsDevTables *tab, const uint8_t *data, size_t dstride, uint8_t *parity, size_t pstride,
                       uint32_t size, size_t count, int num_cu, hipStream_t stream);
 
-/* 32 syndromes (poly form, S_i = c(beta_i)) per codeword into syn, via the
- * remainder of (data || parity) * x^32 mod g and the synt transform */
+/* 32 syndromes (poly form, S_i = c(beta_i)) per codeword into syn: the
+ * encoder's LFSR over the data, XORed with the received parity (E'), and the
+ * synt transform */
 hipError_t rsk_syndrome(const RsDevTables *tab, const uint8_t *data, size_t dstride, const uint8_t *parity,
                         size_t pstride, uint32_t size, size_t count, uint8_t *syn, int num_cu, hipStream_t stream);
 /* the same, also zeroing *reset before any later launch on the stream runs

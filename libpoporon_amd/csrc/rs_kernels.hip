@@ -3,8 +3,11 @@
  *
  * Kernels
  *   rs_lfsr_k<MODE_ENCODE>    parity = m(x) x^32 mod g(x)          (src/encode.c:120-143)
- *   rs_lfsr_k<MODE_SYNDROME>  the 32 syndromes of the received word (src/decode.c:375-415),
- *                             as S_i = r(beta_i) beta_i^-32 with r = c(x) x^32 mod g(x)
+ *   rs_lfsr_k<MODE_SYNDROME>  the 32 syndromes of the received word (src/decode.c:375-415):
+ *                             the received word c = d x^32 + p is the codeword of
+ *                             its data plus E' = p + (d x^32 mod g), so
+ *                             S_i = c(beta_i) = E'(beta_i): 223 LFSR steps (the
+ *                             encode's) instead of 255, then E' -> S by tables
  *   rs_lfsr_k<MODE_CHECK>     the "any syndrome nonzero" flag only
  *   rs_correct_k              erasure locator, Berlekamp-Massey, Chien, Omega,
  *                             Forney, re-syndrome check, apply   (src/decode.c:17-230)
@@ -19,8 +22,8 @@
  * every 16-byte half-row sits in bank slot c, so each ds_read_b128 lane group
  * (16 lanes, one per slot) is conflict-free whatever the data
  * (MI355X_MICROARCH.md, LDS).  The syndrome kernel adds 32 KB of nibble
- * tables that turn the remainder into syndromes with 128 ds_read_b128 per
- * codeword: 160 KB, the whole LDS.
+ * tables that turn E' into syndromes with 128 ds_read_b128 per codeword:
+ * 160 KB, the whole LDS.
  *
  * Correction kernel.  LDS holds (a) the GF(256) exp/log tables replicated 32
  * times so that lane l's ds_read_u8 always hits bank l & 31 (conflict-free
@@ -182,6 +185,23 @@ __device__ __forceinline__ void lfsr_feed(uint32_t (&X)[8], const uint8_t *p, ui
         }
         il_normalize(X, left & 7u);
     }
+}
+
+/* The 32 bytes at p (any alignment) as 8 dwords in order: only aligned
+ * dwords that hold one of them are loaded (no read past the bytes' page). */
+__device__ __forceinline__ void load32_any(uint32_t (&Q)[8], const uint8_t *p)
+{
+    const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+    gu32 *w = reinterpret_cast<gu32 *>(a & ~uintptr_t(3));
+    const uint32_t sh = static_cast<uint32_t>(a & 3u);
+    uint32_t W[9];
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+        W[k] = w[k];
+    W[8] = sh ? w[8] : 0u;
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+        Q[k] = __builtin_amdgcn_alignbyte(W[k + 1], W[k], sh);
 }
 
 /* Where the next codeword's bytes of one stream are: its 16-byte aligned
@@ -358,14 +378,14 @@ __device__ __forceinline__ void store32_any(uint8_t *o, const uint32_t (&P)[8])
 #define PATH_SPLIT 1   /* size 223: data stream (rolling prefetch) + separate parity stream */
 #define PATH_CONTIG 2  /* size 223, parity right after the data: one 255-byte stream (rolling prefetch) */
 
-/* what the kernel does with the final register (remainder bytes P, in order) */
+/* what the kernel does with the final register (encode: the parity bytes P, in order; syndrome / check: E') */
 template <int MODE>
 __device__ __forceinline__ void lfsr_epilogue(const uint32_t (&P)[8], const uint4 *__restrict__ synt, size_t cw,
                                               uint8_t *__restrict__ parity, size_t pstride,
                                               uint8_t *__restrict__ out)
 {
     if (MODE == MODE_SYNDROME) {
-        /* S = sum over remainder bytes m of T_m,lo[r_m & 15] ^ T_m,hi[r_m >> 4] */
+        /* S = sum over the bytes m of E' of T_m,lo[e_m & 15] ^ T_m,hi[e_m >> 4] */
         uint32_t S[8] = {0, 0, 0, 0, 0, 0, 0, 0};
         if ((P[0] | P[1] | P[2] | P[3] | P[4] | P[5] | P[6] | P[7]) != 0u) {
 #pragma unroll
@@ -437,9 +457,14 @@ __global__ __launch_bounds__(LFSR_WG) void rs_lfsr_k(const RsDevTables *__restri
             uint32_t X[8] = {0, 0, 0, 0, 0, 0, 0, 0};
             uint32_t P[8];
             lfsr_feed(X, data + cw * dstride, size, tab);
-            if (MODE != MODE_ENCODE)
-                lfsr_feed(X, parity + cw * pstride, RS_NR, tab);
             il_bytes(P, X, 0);
+            if (MODE != MODE_ENCODE) { /* E' = received parity + parity of the received data */
+                uint32_t Q[8];
+                load32_any(Q, parity + cw * pstride);
+#pragma unroll
+                for (int q = 0; q < 8; ++q)
+                    P[q] ^= Q[q];
+            }
             lfsr_epilogue<MODE>(P, synt, cw, parity, pstride, out);
         }
     } else if (PATH == PATH_CONTIG && MODE != MODE_ENCODE) {
@@ -458,9 +483,17 @@ __global__ __launch_bounds__(LFSR_WG) void rs_lfsr_k(const RsDevTables *__restri
             const NextSrc nx(data + cn * dstride, cn < count, data + cw * dstride);
             if constexpr (!PF)
                 sc.load(NextSrc(data + cw * dstride, true, nullptr));
-            lfsr_stream<FULL_K + RS_NR, 0, 0, 128, PF>(X, sc, nx, tab); /* two loops: each fully unrolled */
-            lfsr_stream<FULL_K + RS_NR, 0, 128, FULL_K + RS_NR, PF>(X, sc, nx, tab);
-            il_bytes(P, X, (FULL_K + RS_NR) & 7);
+            /* the 223 data bytes (two loops, each fully unrolled), then E' =
+             * that parity + the received one (stream bytes 223..254) */
+            lfsr_stream<FULL_K + RS_NR, 0, 0, 128, PF>(X, sc, nx, tab);
+            lfsr_stream<FULL_K + RS_NR, 0, 128, FULL_K - 1, PF>(X, sc, nx, tab);
+            il_step(X, FULL_K - 1, stream_byte(sc, FULL_K - 1), tab);
+            il_bytes(P, X, FULL_K & 7);
+            static_assert(FULL_K % 4 == 3, "parity dword q = bytes 223 + 4q .. 226 + 4q");
+            static_for<0, 8, 1>([&](auto qc) __attribute__((always_inline)) { /* compile-time indices: D stays in registers */
+                constexpr int q = decltype(qc)::value;
+                P[q] ^= __builtin_amdgcn_alignbyte(sc.word(56 + q), sc.word(55 + q), 3);
+            });
             lfsr_epilogue<MODE>(P, synt, cw, parity, pstride, out);
             if constexpr (PF)
                 sc.refill_tail(nx);
@@ -487,8 +520,11 @@ __global__ __launch_bounds__(LFSR_WG) void rs_lfsr_k(const RsDevTables *__restri
                 Stream<RS_NR> sp;
                 sp.load(NextSrc(parity + cw * pstride, true, nullptr));
                 lfsr_stream<FULL_K, 0, 150, FULL_K, PF>(X, sd, dn, tab);
-                lfsr_stream<RS_NR, FULL_K, 0, RS_NR, false>(X, sp, NextSrc(nullptr, false, nullptr), tab);
-                il_bytes(P, X, (FULL_K + RS_NR) & 7);
+                il_bytes(P, X, FULL_K & 7);
+                static_for<0, 8, 1>([&](auto qc) __attribute__((always_inline)) { /* E' = that parity + the received one */
+                    constexpr int q = decltype(qc)::value;
+                    P[q] ^= sp.word(q);
+                });
             } else {
                 lfsr_stream<FULL_K, 0, 0, FULL_K, PF>(X, sd, dn, tab);
                 il_bytes(P, X, FULL_K & 7);
