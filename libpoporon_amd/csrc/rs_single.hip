@@ -659,7 +659,10 @@ __global__ __launch_bounds__(S1_WG) void rs_serve_k(const RsDevTables *__restric
             dec1_body(s, Q, mode, zc + ZC_DATA, zc + ZC_PAR, nullptr, reinterpret_cast<const uint32_t *>(zc + ZC_POS),
                       zc + ZC_CNT, 4u, reinterpret_cast<const uint16_t *>(zc + ZC_EXT), zc + ZC_OK, zc + ZC_COR);
         }
-        __syncthreads(); /* every result store issued before the completion word */
+        /* every wave's result stores (bytes, ok, count: several waves write
+         * them) complete at system scope, then the completion word */
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+        __syncthreads();
         if (t == 0)
             __hip_atomic_store(reinterpret_cast<uint32_t *>(zc + ZC_FLAG), seq, __ATOMIC_RELEASE,
                                __HIP_MEMORY_SCOPE_SYSTEM);
