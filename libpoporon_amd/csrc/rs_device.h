@@ -101,7 +101,7 @@ struct RsCorrParams {
  * device buffer for `cap` codewords (every array 16-byte aligned):
  *   syn   32 B  poly-form syndromes (rsk_syndrome)
  *   lam   16 B  log Lambda_1..16 (255 = zero)            (rsk_bm)
- *   om    16 B  log Omega_0..15, or (RS_ST_FASTB) log B_1..B_16 (255 = zero) (rsk_bm)
+ *   om    16 B  log Omega_0..15 (255 = zero)             (rsk_bm)
  *   roots 32 B  root map over the points alpha^i', i' = 0..255 (rsk_chien),
  *               then the corrections: 16 locations, 16 magnitudes (rsk_forney)
  *   ext   64 B  errata decode (rs_errata.hip): log Lambda_1..32 || log
@@ -118,8 +118,6 @@ struct RsCorrParams {
 #define RS_ST_LIST 2u /* on the list: the general kernel decodes it */
 #define RS_ST_PEND 3u /* erasure mode: left by rs_era_bp_k for the errata kernels */
 #define RS_ST_ERRATA 4u /* errata decode: deg(Lambda) = L (deg & 31), Chien and Forney next */
-#define RS_ST_FASTB 5u /* as RS_ST_FAST, with B_1..B_16 instead of Omega in ws.om (rs_bm_k) */
-#define RS_ST_IS_FAST(st) ((((st) >> 5) & 3u) == 1u) /* RS_ST_FAST or RS_ST_FASTB */
 
 struct RsSplitWs {
     uint8_t *syn, *lam, *om, *roots, *ext, *meta;

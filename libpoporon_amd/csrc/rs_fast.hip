@@ -252,29 +252,10 @@ __global__ __launch_bounds__(BWG, BM_WAVES) void rs_bm_k(const RsDevTables *__re
             deg = (al[i] & 1u) ? (uint32_t)i : deg;
         const bool fast = any && !over && deg == L && deg != 0u;
 
-        /* ---- Omega = S * Lambda mod x^deg (log form), src/decode.c:147-158,
-         * or B in its place ----
-         * After the 32 iterations, at every root x0 of Lambda, Omega(x0) B(x0)
-         * = x0^31 with B in Karn's normalisation (src/decode.c:80-90: Lambda
-         * / its discrepancy at the last lengthening, then shifted): an
-         * identity of the algorithm, checked over fcr 0 / 1 / 5 / 112, prim 1
-         * / 7 / 11 and fast-path miscorrections (tools/probes/bm_b_identity.py).
-         * So where no fast lane of the wave has B past x^16 (`bo`: 16-error
-         * words, whose B has degree <= 32 - L = 16), rs_forney_k takes Omega(x0)
-         * = x0^31 / B(x0) and this kernel skips Omega (~14 % of its lookups).
-         * B_0 = 0 there (the last lengthening is at r <= 31), so B_1..B_16
-         * fill the 16 bytes. */
+        /* ---- Omega = S * Lambda mod x^deg (log form), src/decode.c:147-158 ---- */
         uint32_t ob[4] = {0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
         const uint32_t degmax = wave_max(fast ? deg : 0u);
-        const bool bmode = __ballot(fast && bo != 0u) == 0ull; /* uniform */
-        if (degmax && bmode) {
-            const uint32_t lbp = 255u - (lb >> 7); /* 1 / the discrepancy of B (nonzero) */
-#pragma unroll
-            for (int k = 1; k < NL; ++k) {
-                const uint32_t o = B[k] == AZ ? 255u : red(gf.plog(B[k]) + lbp);
-                ob[(k - 1) >> 2] ^= (o ^ 0xffu) << (8 * ((k - 1) & 3));
-            }
-        } else if (degmax) {
+        if (degmax) {
             /* S_0..S_15 again (L2): keeping them live through BM costs registers */
             const uint4 s4 = any ? reinterpret_cast<const uint4 *>(sp)[0] : make_uint4(0, 0, 0, 0);
             const uint32_t sw[4] = {s4.x, s4.y, s4.z, s4.w};
@@ -319,7 +300,7 @@ __global__ __launch_bounds__(BWG, BM_WAVES) void rs_bm_k(const RsDevTables *__re
                     lb4[(j - 1) >> 2] |= gf.plog(al[j]) << (8 * ((j - 1) & 3));
                 reinterpret_cast<uint4 *>(lamo)[cw] = make_uint4(lb4[0], lb4[1], lb4[2], lb4[3]);
                 reinterpret_cast<uint4 *>(omo)[cw] = make_uint4(ob[0], ob[1], ob[2], ob[3]);
-                meta[cw] = (uint8_t)(((bmode ? RS_ST_FASTB : RS_ST_FAST) << 5) | deg);
+                meta[cw] = (uint8_t)((RS_ST_FAST << 5) | deg);
             }
         }
     }
@@ -377,7 +358,7 @@ __global__ __launch_bounds__(FWG, 8) void rs_chien_k(const RsDevTables *__restri
         const size_t cw = base + threadIdx.x;
         const bool valid = cw < count;
         const uint32_t st = valid ? meta[cw] : 0u;
-        const bool fast = RS_ST_IS_FAST(st);
+        const bool fast = (st >> 5) == RS_ST_FAST;
         if (__ballot(fast) == 0ull)
             continue;
         const uint32_t deg = fast ? (st & 31u) : 0u;
@@ -525,11 +506,9 @@ __global__ __launch_bounds__(F2WG, 6) void rs_forney_k(const RsDevTables *__rest
         const size_t cw = base + threadIdx.x;
         const bool valid = cw < count;
         const uint32_t st = valid ? meta[cw] : 0u;
-        const bool fast = RS_ST_IS_FAST(st);
+        const bool fast = (st >> 5) == RS_ST_FAST;
         if (__ballot(fast) == 0ull)
             continue;
-        const bool isb = (st >> 5) == RS_ST_FASTB; /* ws.om holds B_1..B_16: Omega(x0) = x0^31 / B(x0) */
-        const bool bwave = __ballot(fast && isb) != 0ull;
         const uint32_t deg = fast ? (st & 31u) : 0u;
         uint4 o4 = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu), l4 = o4;
         uint32_t rl[4] = {0, 0, 0, 0};
@@ -586,22 +565,16 @@ __global__ __launch_bounds__(F2WG, 6) void rs_forney_k(const RsDevTables *__rest
                 num[t] ^= gf.expa(gf.loga(nh[t]) + s[t]);
                 den[t] ^= gf.expa(gf.loga(dh[t]) + s[t]);
                 uint32_t mag;
-                if (fcr1 && !bwave) {
+                if constexpr (fcr1) {
                     /* alpha^(log num + 255 - log den) straight from the address
                      * forms: 128 (log num - log den + 255) + pofs is inside the
                      * exp table's two periods (den != 0 at the distinct roots of
                      * the fast path) */
                     mag = gf.expa(gf.loga(num[t]) - gf.loga(den[t]) + mp);
                 } else {
-                    const uint32_t ln2 =
-                        fcr1 ? 0u : mod255((uint32_t)((int32_t)ir[t] * ((int32_t)P.fcr - 1) + (int32_t)RS_NN));
+                    const uint32_t ln2 = mod255((uint32_t)((int32_t)ir[t] * ((int32_t)P.fcr - 1) + (int32_t)RS_NN));
                     const uint32_t lden = gf.plog(gf.loga(den[t])); /* log 0 = 255 in the reference: no den = 0 guard */
-                    const uint32_t lq = gf.plog(gf.loga(num[t]));
-                    /* B lanes: num = sum B_(m+1) x0^m = B(x0) / x0, never 0 at a
-                     * root, so log Omega(x0) = 31 i - log B(x0) = 30 i - log num */
-                    const uint32_t i0 = ir[t] == 255u ? 0u : ir[t];
-                    const uint32_t ln = isb ? mod255(30u * i0 + 255u - lq) : lq;
-                    mag = gf.exp(red(ln + ln2 + RS_NN - lden));
+                    mag = gf.exp(red(gf.plog(gf.loga(num[t])) + ln2 + RS_NN - lden));
                 }
                 const bool z = (uint32_t)(n0 + t) < deg && num[t] != 0u;
                 fixed += z ? 1u : 0u;
@@ -856,7 +829,7 @@ __global__ __launch_bounds__(AWG) void rs_apply_k(const uint8_t *__restrict__ me
         return;
     const size_t cw = base + lane;
     const bool valid = cw < count;
-    const bool fast = valid && RS_ST_IS_FAST(meta[cw]);
+    const bool fast = valid && (meta[cw] >> 5) == RS_ST_FAST;
     uint32_t pw[NW], mw[NW];
 #pragma unroll
     for (int k = 0; k < NW; ++k)
