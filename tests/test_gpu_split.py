@@ -143,6 +143,47 @@ def test_split_device_strides(monkeypatch, oracle_default, offset, stride):
     assert (out[:, 255:] == 0).all()  # bytes between rows untouched
 
 
+@pytest.mark.parametrize("path", ["split", "single"])
+@pytest.mark.parametrize("size", [223, 150])
+def test_device_separate_parity(monkeypatch, oracle_default, path, size):
+    """Data and parity in separate device buffers at odd offsets and strides
+    (the syndrome kernel's two-stream path for size 223, its any-alignment
+    path for shortened codes): the received parity XORed into the data's
+    LFSR parity at every alignment."""
+    import torch
+    h = _handle(monkeypatch, path)
+    rng = np.random.default_rng(size)
+    n = 20000
+    data = rng.integers(0, 256, (n, size), dtype=np.uint8)
+    par = oracle_default.encode_batch(data)
+    for c in range(n):
+        ne = int(rng.integers(0, 19))
+        pos = rng.permutation(size + 32)[:ne]
+        mag = rng.integers(1, 256, ne, dtype=np.uint8)
+        for p, m in zip(pos, mag):
+            if p < size:
+                data[c, p] ^= m
+            else:
+                par[c, p - size] ^= m
+    want = oracle_default.decode_batch(data, par)
+    ds, ps, do, po = size + 5, 35, 1, 3
+    dbuf = np.zeros(do + n * ds, np.uint8)
+    pbuf = np.zeros(po + n * ps, np.uint8)
+    dbuf[do:].reshape(n, ds)[:, :size] = data
+    pbuf[po:].reshape(n, ps)[:, :32] = par
+    dd, dp = torch.from_numpy(dbuf).cuda(), torch.from_numpy(pbuf).cuda()
+    ok = torch.zeros(n, dtype=torch.uint8, device="cuda")
+    cor = torch.zeros(n, dtype=torch.uint8, device="cuda")
+    s = torch.cuda.current_stream().cuda_stream
+    h.decode_batch_device(dd.data_ptr() + do, ds, dp.data_ptr() + po, ps, size, n, ok.data_ptr(), cor.data_ptr(),
+                          stream=s)
+    torch.cuda.synchronize()
+    gd = dd.cpu().numpy()[do:].reshape(n, ds)
+    gp = dp.cpu().numpy()[po:].reshape(n, ps)
+    _same((ok.cpu().numpy(), cor.cpu().numpy(), gd[:, :size], gp[:, :32]), want)
+    assert not gd[:, size:].any() and not gp[:, 32:].any()
+
+
 def test_split_kernels_timed(monkeypatch, torch_cuda_split):
     """A 2^16 batch with 16 errors each runs the split kernels (timing ids
     1, 4..8) and not the single kernel; the list kernel finds nothing to do."""
