@@ -33,6 +33,12 @@ for step in "$@"; do
     batchlat) run batchlat 300 python tools/batch_latency.py
               POPORON_AMD_DECODE_PATH=split run batchlat_split 300 python tools/batch_latency.py
               POPORON_AMD_DECODE_PATH=wave run batchlat_wave 300 python tools/batch_latency.py ;;
+    latab) # single-call latency of each build/*.so, alternated twice (same box)
+        for pass in 1 2; do
+            for so in build/*.so; do
+                POPORON_AMD_LIB=$so run "latab_$(basename $so .so)_$pass" 200 python tools/lat_single.py 2000
+            done
+        done ;;
     ab) # A/B of the experiment builds in build/*.so, alternated twice (same box)
         run ab 900 python tools/exp_bench.py $(ls build/*.so) $(ls build/*.so) ;;
     prof) run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- \
