@@ -179,7 +179,10 @@ __global__ __launch_bounds__(S1_WG) void rs_enc1_k(const RsDevTables *__restrict
     fill_tabs(s, T, t);
     enc1_body(s, wred, T, data, parity, size);
     if (flag) {
-        __syncthreads(); /* every parity store issued before the flag */
+        /* every wave's parity stores acknowledged, then lane 0's system-scope
+         * release and the flag (rs_serve_k) */
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
         if (t == 0)
             __hip_atomic_store(flag, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     }
@@ -565,7 +568,8 @@ __global__ __launch_bounds__(S1_WG) void rs_dec1_k(const RsDevTables *__restrict
     fill_tabs(s.g, T, t);
     dec1_body(s, P, mode, data, parity, pos8, pos32, cnt, cnt_bytes, ext, okp, corp);
     if (flag) {
-        __syncthreads(); /* every result store issued before the flag */
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); /* as rs_enc1_k */
+        __syncthreads();
         if (t == 0)
             __hip_atomic_store(flag, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     }
