@@ -869,9 +869,12 @@ def host_pipeline(be, w, reps=3):
         td.append(time.perf_counter() - t0)
     assert ok.all() and (cor == 16).all() and (work == host).all()
     e, d = min(te), min(td)
+    idx = np.arange(0, B, SAMPLE_STRIDE)  # the parity sample of this API's own outputs
     return {"encode_cw_per_s": round(B / e, 1), "encode_GB_per_s_pcie": round(B * (K + NR) / e / 1e9, 2),
             "decode_cw_per_s": round(B / d, 1), "decode_GB_per_s_pcie": round(B * (2 * N + 2) / d / 1e9, 2),
-            "codewords": B, "note": "host-memory batch API, PCIe-inclusive (best of %d); not `value`" % reps}
+            "codewords": B, "note": "host-memory batch API, PCIe-inclusive (best of %d); not `value`" % reps,
+            "_samples": {"host_encode": {"msg": msgs[idx], "got_par": par[idx]},
+                         "host_decode16": {"in": bad[idx], "out": work[idx], "ok": ok[idx], "cor": cor[idx]}}}
 
 
 def call_latency(be, calls=2000):
@@ -1151,7 +1154,9 @@ def main(argv=None):
                                if traffic else tnote),
         })
         if world == 1 and not args.no_host:
-            line["host_pipeline"] = host_pipeline(be, w)
+            hp = host_pipeline(be, w)
+            samples.update(hp.pop("_samples"))
+            line["host_pipeline"] = hp
         if world == 1 and not args.no_latency:
             line["single_call_latency"] = call_latency(be)
     else:
