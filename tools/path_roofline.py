@@ -14,7 +14,7 @@ mode the errata kernels only take their early exit) and erasure32 otherwise
 -- the same kernel sets bench.py sums per mode (bench.PATHS).  A path's time
 is the mean over its instances of the sum of their dispatch durations;
 achieved = 255 B x n / that time, frac = achieved / 8 TB/s.
-(A `*_kernel_stats.csv` cannot separate rs_era_k's two roles: 32 sorted
+(A `*_kernel_stats.csv` cannot separate rs_era_bp_k's two roles: 32 sorted
 erasures in erasure32, the 16-us hand-off in errata16e8.)
 """
 import argparse
