@@ -43,6 +43,18 @@ for step in "$@"; do
         run ab 900 python tools/exp_bench.py $(ls build/*.so) $(ls build/*.so) ;;
     prof) run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- \
         python3 bench.py --no-cpu-baseline --no-host --no-c4 --no-latency --no-mixed --steps 10 ;;
+    pmc_era)
+        # the erasure / errata kernels: the same counter groups on the driver's erasure and errata modes
+        i=0
+        for mode in erasure errata; do
+            for grp in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE" \
+                       "SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAIT_ANY" \
+                       "SQ_INSTS_SMEM SQ_INSTS_BRANCH SQ_IFETCH SQ_ACTIVE_INST_LDS SQ_INST_CYCLES_SALU SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS"; do
+                run pmc_${mode}_$i 300 rocprofv3 --pmc $grp -d gpurun_out/pmcera/pmc_${mode}_$i -o pmc --output-format csv -- \
+                    python3 tools/kernel_driver.py --mode $mode --reps 3
+                i=$((i+1))
+            done
+        done ;;
     pmc)
         # one rocprofv3 pass per counter group (never combined with tracing)
         i=0
