@@ -509,11 +509,15 @@ class Multi:
                     "poporon_encode_batch_multi_device")
 
     def decode_batch_device(self, d_data, data_stride, d_parity, parity_stride, size, count, d_ok, d_corrected=None,
-                            streams=None):
+                            streams=None, d_positions=None, positions_stride=0, d_counts=None):
+        """d_positions / d_counts (erasure batches): one pointer per device, as d_data."""
         G = self.devices
         arr = lambda v: (C.c_void_p * G)(*v)  # noqa: E731
         self._check(self.lib.poporon_decode_batch_multi_device(self.h, arr(d_data), data_stride, arr(d_parity),
-                                                               parity_stride, size, count, None, 0, None, arr(d_ok),
+                                                               parity_stride, size, count,
+                                                               arr(d_positions) if d_positions else None,
+                                                               positions_stride,
+                                                               arr(d_counts) if d_counts else None, arr(d_ok),
                                                                arr(d_corrected) if d_corrected else None,
                                                                arr(streams) if streams else None),
                     "poporon_decode_batch_multi_device")

@@ -147,6 +147,7 @@ struct GpuCtx {
     hipStream_t sstream = nullptr;
     bool srv_on = false;
     uint32_t srv_id = 0;
+    uint32_t srv_seq = 0; /* request words of the server (its own count: zc_seq also moves without it) */
     size_t stage_cap = 0;
     /* host-batch pipeline: PIPE_SLOTS chunks in flight, one stream each */
     struct PipeSlot {
@@ -702,6 +703,18 @@ EXPORT poporon_t *poporon_create(const poporon_config_t *config)
     return h;
 }
 
+/* The next request word of the single-call server (rs_serve_k): a new
+ * sequence number, and never the word the server saw last -- it acts on a
+ * change of the word only (14 bits of sequence wrap). */
+static uint32_t srv_word(GpuCtx &g, uint32_t prev, uint32_t op, uint32_t size, uint32_t mode)
+{
+    uint32_t w;
+    do
+        w = ZC_REQ_WORD(++g.srv_seq, op, size, mode);
+    while (w == prev);
+    return w;
+}
+
 /* Frees whatever the context holds, ready or not: a gpu_init that failed
  * half-way leaves a stream or tables behind, and they go here so that the
  * next call retries from scratch. */
@@ -740,7 +753,7 @@ static void gpu_release(GpuCtx &g)
     if (g.sstream) {
         if (g.zc && g.srv_on) { /* ask a live server to leave now rather than at its idle limit */
             volatile uint32_t *req = reinterpret_cast<volatile uint32_t *>(g.zc + ZC_REQ);
-            *req = ZC_REQ_WORD(g.zc_seq + 1u, RS_SRV_STOP, 0u, 0u);
+            *req = srv_word(g, *req, RS_SRV_STOP, 0u, 0u);
         }
         (void)hipStreamSynchronize(g.sstream);
         (void)hipStreamDestroy(g.sstream);
@@ -855,6 +868,18 @@ static bool gpu_init(poporon_t *h)
     gpu_release(h->gpu);
     g_last_error = msg;
     return false;
+}
+
+/* the single-call server (below) leaves before a batch call on its handle:
+ * while resident it holds a CU (and, with few hardware queues, may sit ahead of
+ * the batch's dispatches) */
+static bool srv_stop(poporon_t *h);
+
+/* every batch entry point: the device context, and no live server of this
+ * handle beside the batch's kernels */
+static bool batch_enter(poporon_t *h)
+{
+    return gpu_init(h) && srv_stop(h);
 }
 
 static bool gpu_init_steps(poporon_t *h)
@@ -1343,7 +1368,7 @@ EXPORT bool poporon_check_batch_device(poporon_t *h, const uint8_t *d_data, size
         return fail("poporon_check_batch_device serves RS handles");
     if (!check_decode_size(h, size))
         return fail("size %zu outside [1, %u]", size, (unsigned)kmax(h));
-    if (!gpu_init(h))
+    if (!batch_enter(h))
         return false;
     DeviceGuard dg(h->gpu.device);
     hipStream_t s = (hipStream_t)stream;
@@ -1374,7 +1399,7 @@ EXPORT bool poporon_syndrome_batch_device(poporon_t *h, const uint8_t *d_data, s
         return fail("syndrome_stride < num_roots (%u)", (unsigned)h->rs->num_roots);
     if (!check_decode_size(h, size))
         return fail("size %zu outside [1, %u]", size, (unsigned)kmax(h));
-    if (!gpu_init(h))
+    if (!batch_enter(h))
         return false;
     DeviceGuard dg(h->gpu.device);
     hipStream_t s = (hipStream_t)stream;
@@ -1406,7 +1431,7 @@ EXPORT bool poporon_encode_batch_device(poporon_t *h, const uint8_t *d_data, siz
         return fail("NULL argument");
     if (!check_encode_size(h, size))
         return false;
-    if (!gpu_init(h))
+    if (!batch_enter(h))
         return false;
     DeviceGuard dg(h->gpu.device);
     return launch_encode(h, d_data, data_stride, d_parity, parity_stride, size, count, (hipStream_t)stream);
@@ -1423,7 +1448,7 @@ EXPORT bool poporon_decode_batch_device(poporon_t *h, uint8_t *d_data, size_t da
         return fail("erasure batch needs an RS handle, counts and positions_stride >= num_roots");
     if (!check_decode_size(h, size))
         return fail("decode size %zu outside [1, %u]", size, (unsigned)kmax(h));
-    if (!gpu_init(h))
+    if (!batch_enter(h))
         return false;
     DeviceGuard dg(h->gpu.device);
     return launch_decode(h, d_data, data_stride, d_parity, parity_stride, size, count, nullptr, 0, d_positions,
@@ -1443,7 +1468,7 @@ EXPORT bool poporon_decode_batch_syndrome_device(poporon_t *h, uint8_t *d_data, 
         return fail("syndrome_stride < num_roots (%u)", (unsigned)h->rs->num_roots);
     if (!check_decode_size(h, size))
         return fail("decode size %zu outside [1, %u]", size, (unsigned)kmax(h));
-    if (!gpu_init(h))
+    if (!batch_enter(h))
         return false;
     DeviceGuard dg(h->gpu.device);
     return launch_decode(h, d_data, data_stride, d_parity, parity_stride, size, count, d_syndromes, syndrome_stride,
@@ -1533,7 +1558,7 @@ EXPORT bool poporon_encode_batch(poporon_t *h, const uint8_t *data, size_t data_
         return fail("NULL argument");
     if (!check_encode_size(h, size))
         return false;
-    if (!gpu_init(h))
+    if (!batch_enter(h))
         return false;
     DeviceGuard dg(h->gpu.device);
     GpuCtx &g = h->gpu;
@@ -1588,7 +1613,7 @@ EXPORT bool poporon_decode_batch(poporon_t *h, uint8_t *data, size_t data_stride
         return fail("erasure batch needs an RS handle, counts and positions_stride >= num_roots");
     if (!check_decode_size(h, size))
         return fail("decode size %zu outside [1, %u]", size, (unsigned)kmax(h));
-    if (!gpu_init(h))
+    if (!batch_enter(h))
         return false;
     DeviceGuard dg(h->gpu.device);
     GpuCtx &g = h->gpu;
@@ -1722,14 +1747,11 @@ EXPORT poporon_multi_t *poporon_amd_multi_create(const poporon_config_t *config,
     poporon_multi_t *m = new (std::nothrow) _poporon_multi_t();
     if (!m)
         return nullptr;
+    /* a device may be listed more than once: its handles are independent
+     * (own tables, workspace, streams and host threads) and share that GPU --
+     * e.g. two host pipelines per device, or the G > 1 split exercised on a
+     * one-GPU machine (tests/test_gpu_fullsize.py) */
     for (size_t i = 0; i < devs.size(); i++) {
-        for (size_t j = 0; j < i; j++) {
-            if (devs[j] == devs[i]) {
-                fail("device %d listed twice", devs[i]);
-                poporon_amd_multi_destroy(m);
-                return nullptr;
-            }
-        }
         poporon_t *p = poporon_create(config);
         if (!p || !poporon_amd_set_device(p, devs[i]) || !gpu_init(p)) {
             const std::string msg = g_last_error;
@@ -1929,10 +1951,8 @@ static bool srv_call(poporon_t *h, uint32_t op, uint32_t size, uint32_t mode)
 {
     GpuCtx &g = h->gpu;
     volatile uint32_t *z32 = reinterpret_cast<volatile uint32_t *>(g.zc);
-    const uint32_t seq = ++g.zc_seq;
-    /* the request word differs from the last one the server served (their
-     * sequence numbers differ: 14 bits, one request in flight at a time) */
-    const uint32_t prev = z32[ZC_REQ / 4], word = ZC_REQ_WORD(seq, op, size, mode);
+    /* the request word differs from the last one the server saw */
+    const uint32_t prev = z32[ZC_REQ / 4], word = srv_word(g, prev, op, size, mode);
     z32[ZC_FLAG / 4] = 0u; /* the server answers with the request word (never 0: op >= 1) */
     std::atomic_thread_fence(std::memory_order_release); /* the payload before the request word */
     z32[ZC_REQ / 4] = word;
@@ -1970,6 +1990,43 @@ static bool srv_call(poporon_t *h, uint32_t op, uint32_t size, uint32_t mode)
         __builtin_ia32_pause();
 #endif
     }
+}
+
+/* A live server of this handle leaves now (a stop request, then its exit
+ * word: one PCIe round trip).  Batch calls come here first (batch_enter): a
+ * resident server holds one CU's LDS, so one workgroup of a persistent batch
+ * grid would wait for its idle limit, and with GPU_MAX_HW_QUEUES below the
+ * streams in use its dispatch can share a hardware queue with the batch's.
+ * The next single call launches a new server. */
+static bool srv_stop(poporon_t *h)
+{
+    GpuCtx &g = h->gpu;
+    if (!g.srv_on || !g.zc)
+        return true;
+    volatile uint32_t *z32 = reinterpret_cast<volatile uint32_t *>(g.zc);
+    const uint32_t prev = z32[ZC_REQ / 4];
+    std::atomic_thread_fence(std::memory_order_release);
+    z32[ZC_REQ / 4] = srv_word(g, prev, RS_SRV_STOP, 0u, 0u);
+    const volatile uint32_t *ex = z32 + ZC_EXITED / 4;
+    for (uint32_t spin = 1; *ex != g.srv_id; ++spin) {
+        if ((spin & 4095u) == 0u) {
+            const hipError_t e = hipStreamQuery(g.sstream);
+            if (e == hipSuccess && *ex != g.srv_id) {
+                g.srv_on = false;
+                return fail("single-call server ended without its exit word");
+            }
+            if (e != hipSuccess && e != hipErrorNotReady) {
+                g.srv_on = false;
+                return fail("HIP error %d (%s) in the single-call server", (int)e, hipGetErrorString(e));
+            }
+        }
+#if defined(__x86_64__)
+        __builtin_ia32_pause();
+#endif
+    }
+    std::atomic_thread_fence(std::memory_order_acquire);
+    g.srv_on = false;
+    return true;
 }
 
 EXPORT bool poporon_encode(poporon_t *h, uint8_t *data, size_t size, uint8_t *parity)

@@ -738,10 +738,12 @@ __global__ __launch_bounds__(COR_WG) void rs_correct_k(const RsDevTables *__rest
     const Gf gf{lds_addr(lgf) + (threadIdx.x & (GF_REPL - 1)) * 4 + 1};
     uint8_t *srow = lsyn + threadIdx.x;
 
-    /* The trip count is uniform per workgroup and the whole wave enters the
-     * correction when any of its codewords needs it (the rest, with zero
-     * syndromes, ride through BM as no-ops and leave at deg = 0): the BM
-     * bounds are then full-wave DPP reductions. */
+    /* Runs of 64 codewords are dealt per wave, so the trip count is uniform
+     * per wave only -- waves of one workgroup may make different numbers of
+     * passes, and no workgroup barrier may appear inside this loop.  The whole
+     * wave enters the correction when any of its codewords needs it (the
+     * rest, with zero syndromes, ride through BM as no-ops and leave at
+     * deg = 0): the BM bounds are then full-wave DPP reductions. */
     const uint32_t wslot = threadIdx.x >> 6, lane = threadIdx.x & 63u;
     for (size_t run = (size_t)wslot * gridDim.x + blockIdx.x; run * 64u < n; run += (size_t)(COR_WG / 64) * gridDim.x) {
         const size_t idx = run * 64u + lane; /* the wave's run of 64 codewords: the trip count is wave-uniform */

@@ -271,6 +271,95 @@ def test_multi_device_api(oracle_default, torch_cuda):
     m.close()
 
 
+def _mixed_channel(rng, n):
+    """Codewords with errors only (even c: 0..19 errors, past t as well) and
+    erasure rows (odd c: 0, 8, 16 or 32 sorted slots in the data, plus errors
+    within 2e + era <= 32); slots past the count stay 0 (read by the
+    reference as stale entries, quirk Q2)."""
+    data = rng.integers(0, 256, (n, K), dtype=np.uint8)
+    slots = np.zeros((n, NR), np.uint8)
+    cnts = np.zeros(n, np.uint8)
+    errs = []
+    for c in range(n):
+        era = (0, 8, 16, 32)[(c >> 1) % 4] if c % 2 else 0
+        if era:
+            slots[c, :era] = np.sort(rng.choice(K, era, replace=False))
+            cnts[c] = era
+        ne = (NR - era) // 2 if c % 2 else c % 20
+        errs.append((era, ne))
+    return data, slots, cnts, errs
+
+
+@pytest.mark.parametrize("G", [2, 4, 8])
+def test_multi_device_repeated(oracle_default, torch_cuda, G):
+    """The multi-device C ABI at G > 1 on one GPU: G independent handles on
+    device 0, each taking its contiguous range (poporon_amd_multi_range), the
+    host entry points with one host thread per handle and the device entry
+    points with per-handle shards and streams.  Bytes, ok and corrected_num
+    equal the oracle's for error and erasure batches.  At G = 2 each handle's
+    range (20,000 codewords) takes the split kernels, at G = 4 / 8 (10,000 /
+    5,000) the one-codeword-per-wave kernel."""
+    torch = torch_cuda
+    m = P.Multi(devices=[0] * G)
+    assert m.devices == G
+    n = 80000
+    rng = np.random.default_rng(500 + G)
+    data, slots, cnts, errs = _mixed_channel(rng, n)
+    par = m.encode_batch(data)
+    assert (par == oracle_default.encode_batch(data)).all()
+    cw = np.concatenate([data, par], 1)
+    for c, (era, ne) in enumerate(errs):
+        for s in slots[c, :era]:
+            cw[c, s] ^= rng.integers(1, 256, dtype=np.uint8)
+        free = np.setdiff1d(np.arange(N), slots[c, :era]) if era else np.arange(N)
+        p = rng.permutation(free)[:ne]
+        cw[c, p] ^= rng.integers(1, 256, ne, dtype=np.uint8)
+    plain, era_rows = np.arange(0, n, 2), np.arange(1, n, 2)
+    # host entry points: errors only, then erasure rows
+    ok, cor, d, p = m.decode_batch(cw[plain, :K], cw[plain, K:])
+    ook, ocor, od, op = oracle_default.decode_batch(cw[plain, :K], cw[plain, K:])
+    assert (ok == ook).all() and (cor == ocor).all() and (d == od).all() and (p == op).all()
+    ok, cor, d, p = m.decode_batch(cw[era_rows, :K], cw[era_rows, K:], slots[era_rows], cnts[era_rows])
+    eok, ecor, ed, ep = oracle_default.decode_batch(cw[era_rows, :K], cw[era_rows, K:],
+                                                    slots[era_rows].astype(np.uint32), cnts[era_rows].astype(np.uint32))
+    assert (ok == eok).all() and (cor == ecor).all() and (d == ed).all() and (p == ep).all()
+    assert int(eok.sum()) == len(era_rows)
+    # device entry points: handle i's shard of the rows on device 0, its own stream
+    streams = [torch.cuda.Stream() for _ in range(G)]
+    for rows, pos, oracle_out in ((plain, None, (ook, ocor, od, op)), (era_rows, slots, (eok, ecor, ed, ep))):
+        nn = len(rows)
+        shards, msgs, oks, cors, poss, cnss = [], [], [], [], [], []
+        for i in range(G):
+            lo, hi = P.shard_range(nn, i, G)
+            shards.append(torch.from_numpy(np.ascontiguousarray(cw[rows[lo:hi]])).cuda())
+            msgs.append(torch.from_numpy(np.ascontiguousarray(cw[rows[lo:hi], :K])).cuda())
+            oks.append(torch.zeros(hi - lo, dtype=torch.uint8, device="cuda"))
+            cors.append(torch.zeros(hi - lo, dtype=torch.uint8, device="cuda"))
+            if pos is not None:
+                poss.append(torch.from_numpy(np.ascontiguousarray(pos[rows[lo:hi]])).cuda())
+                cnss.append(torch.from_numpy(np.ascontiguousarray(cnts[rows[lo:hi]])).cuda())
+        pars = [torch.zeros((t.shape[0], NR), dtype=torch.uint8, device="cuda") for t in msgs]
+        torch.cuda.synchronize()
+        m.encode_batch_device([t.data_ptr() for t in msgs], K, [t.data_ptr() for t in pars], NR, K, nn,
+                              [s.cuda_stream for s in streams])
+        kw = {}
+        if pos is not None:
+            kw = dict(d_positions=[t.data_ptr() for t in poss], positions_stride=NR,
+                      d_counts=[t.data_ptr() for t in cnss])
+        m.decode_batch_device([t.data_ptr() for t in shards], N, [t.data_ptr() + K for t in shards], N, K, nn,
+                              [o.data_ptr() for o in oks], [c.data_ptr() for c in cors],
+                              streams=[s.cuda_stream for s in streams], **kw)
+        torch.cuda.synchronize()
+        want_par = np.concatenate([oracle_default.encode_batch(t.cpu().numpy()) for t in msgs])
+        assert (np.concatenate([t.cpu().numpy() for t in pars]) == want_par).all()
+        out = np.concatenate([t.cpu().numpy() for t in shards])
+        w_ok, w_cor, w_d, w_p = oracle_out
+        assert (np.concatenate([o.cpu().numpy() for o in oks]) == w_ok).all()
+        assert (np.concatenate([c.cpu().numpy() for c in cors]) == w_cor).all()
+        assert (out[:, :K] == w_d).all() and (out[:, K:] == w_p).all()
+    m.close()
+
+
 # ---------------------------------------------------------------------------
 # compiled C drop-in programs (tests/c): the reference's README example and
 # its RS codec assertions, linked against libpoporon_amd.so

@@ -238,3 +238,41 @@ def test_single_call_server_idle_and_relaunch(oracle_default):
         assert ok and n == 16 and (d == msgs[c]).all() and (q == want[c]).all(), c
     h.close()  # asks a live server to leave at once
     assert (h2.encode(msgs[0]) == want[0]).all()
+
+
+def test_batch_after_single_call(oracle_default):
+    """A device batch issued right after a single call: the batch entry point
+    first asks the handle's live server to leave (api.cpp srv_stop), so the
+    batch is not left waiting for the CU the server holds.  Results equal the
+    ones without a single call before them, and the batch takes no longer
+    than 1.5x + 0.2 ms of that (tools/server_batch.py measures the same)."""
+    import time
+
+    import torch
+    _need_gpu()
+    h = P.Poporon.default()
+    n = 1 << 20
+    rng = np.random.default_rng(9)
+    msgs = torch.from_numpy(rng.integers(0, 256, (n, 223), dtype=np.uint8)).cuda()
+    par = torch.zeros((n, NR), dtype=torch.uint8, device="cuda")
+    one = msgs[0].cpu().numpy()
+    want_one = oracle_default.encode_batch(one[None])[0]
+    s = torch.cuda.current_stream().cuda_stream
+    times = {True: [], False: []}
+    ref = None
+    for r in range(12):
+        after = bool(r % 2)
+        if after:
+            assert (h.encode(one) == want_one).all()  # the server is resident now
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        h.encode_batch_device(msgs.data_ptr(), 223, par.data_ptr(), NR, 223, n, s)
+        torch.cuda.synchronize()
+        times[after].append(time.perf_counter() - t0)
+        if ref is None:
+            ref = par.clone()
+        assert torch.equal(par, ref), r
+    sample = msgs[::4096].cpu().numpy()
+    assert (oracle_default.encode_batch(sample) == ref[::4096].cpu().numpy()).all()
+    alone, after = np.median(times[False][1:]), np.median(times[True][1:])
+    assert after <= 1.5 * alone + 2e-4, (alone, after)

@@ -232,7 +232,10 @@ PTU_EXPORT double ptu_time_decode(void *fn, void *h, uint8_t *data, uint64_t dst
     for (uint64_t c = 0; c < calls; ++c) {
         size_t n = 0;
         ok[c] = dec(h, data + c * dstride, size, par + c * pstride, &n) ? 1 : 0;
-        cor[c] = (uint8_t)n;
+        /* a device failure (corrected_num = POPORON_AMD_DEVICE_ERROR, past
+         * every count the reference reports) is recorded as 255, never
+         * truncated into an ordinary count */
+        cor[c] = n > 254u ? (uint8_t)255u : (uint8_t)n;
     }
     return std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
 }
