@@ -39,6 +39,11 @@ for step in "$@"; do
                 POPORON_AMD_LIB=$so run "latab_$(basename $so .so)_$pass" 200 python tools/lat_single.py 2000
             done
         done ;;
+    srvbatch) # batch calls right after a single call, each build in build/*.so (+ the server off)
+        for so in build/*.so; do
+            POPORON_AMD_LIB=$so run "srvbatch_$(basename $so .so)" 200 python tools/server_batch.py
+        done
+        POPORON_AMD_SERVE=0 run srvbatch_noserve 200 python tools/server_batch.py ;;
     ab) # A/B of the experiment builds in build/*.so, alternated twice (same box)
         run ab 900 python tools/exp_bench.py $(ls build/*.so) $(ls build/*.so) ;;
     prof) run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- \
