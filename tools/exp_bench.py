@@ -16,7 +16,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 for lib in sys.argv[1:]:
     env = dict(os.environ, POPORON_AMD_LIB=os.path.abspath(lib))
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--no-cpu-baseline", "--no-host", "--no-c4",
-                        "--no-latency", "--no-mixed", "--steps", "6"], env=env, capture_output=True, text=True, timeout=300, cwd=ROOT)
+                        "--no-latency", "--no-mixed", "--no-general", "--steps", "6"], env=env, capture_output=True, text=True, timeout=300, cwd=ROOT)
     line = [x for x in r.stdout.splitlines() if x.startswith("{")]
     if not line:
         print(os.path.basename(lib), "FAILED", r.stderr[-400:], flush=True)

@@ -47,7 +47,7 @@ for step in "$@"; do
     ab) # A/B of the experiment builds in build/*.so, alternated twice (same box)
         run ab 900 python tools/exp_bench.py $(ls build/*.so) $(ls build/*.so) ;;
     prof) run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- \
-        python3 bench.py --no-cpu-baseline --no-host --no-c4 --no-latency --no-mixed --steps 10 ;;
+        python3 bench.py --no-cpu-baseline --no-host --no-c4 --no-latency --no-mixed --no-general --steps 10 ;;
     pmc_era)
         # the erasure / errata kernels: the same counter groups on the driver's erasure and errata modes
         i=0
