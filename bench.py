@@ -86,6 +86,7 @@ def parse_args(argv=None):
     ap.add_argument("--no-mixed", action="store_true", help="skip the mixed-channel decode (binomial error counts)")
     ap.add_argument("--no-host", action="store_true", help="skip the host-memory (PCIe) pipeline rates")
     ap.add_argument("--no-latency", action="store_true", help="skip the single-codeword call latency")
+    ap.add_argument("--no-general", action="store_true", help="skip the general-parameter RS(255,239) line")
     ap.add_argument("--backend", default="", help="tests only: module with a CPU Backend (see docstring)")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic_latest.json"),
                     help="HBM bytes per codeword of each path from rocprofv3 --pmc passes (tools/pmc_traffic.py), "
@@ -877,6 +878,69 @@ def host_pipeline(be, w, reps=3):
                          "host_decode16": {"in": bad[idx], "out": work[idx], "ok": ok[idx], "cor": cor[idx]}}}
 
 
+def general_params(be, n=1 << 20, reps=5, params=(8, 0x11D, 1, 1, 16), nerr=8):
+    """SURVEY 8(f) row 1, the general-parameter kernels (rs_generic.hip: one
+    codeword per lane, per-lane arrays in LDS): RS(255, 239) -- the default
+    field with 16 roots, which the RS(255,223) kernels do not serve -- encode of
+    n resident messages and decode with t = 8 random errors per codeword, wall
+    time per call (stream-synchronised, median of reps).  Every 4096th codeword
+    is compared with the oracle restatement (oracle/rs_oracle.c, pinned to the
+    compiled reference's golden vectors for 13 parameter sets)."""
+    import numpy as np
+
+    from oracle import Oracle
+    torch, P, T = be.torch, be.P, be.T
+    m, poly, fcr, prim, nr = params
+    k = 255 - nr
+    h = P.Poporon(m, poly, fcr, prim, nr, device=be.local)
+    s = be.stream
+    rows = torch.empty((n, N), dtype=torch.uint8, device=be.dev)
+    T.synth_rows(SEED + 40, 0, n, k, rows.data_ptr(), N, s)
+    b = rows.data_ptr()
+    h.encode_batch_device(b, N, b + k, N, k, n, s)  # warm-up
+    te = []
+    for _ in range(reps):
+        be.sync()
+        t0 = time.perf_counter()
+        h.encode_batch_device(b, N, b + k, N, k, n, s)
+        be.sync()
+        te.append(time.perf_counter() - t0)
+    clean = rows.clone()
+    pos, mag = be.errors(0, n, nerr, N, SEED + 41)
+    bad = clean.clone()
+    T.channel_xor(pos.data_ptr(), mag.data_ptr(), nerr, bad.data_ptr(), N, n, s)
+    ok, cor = be.status(n)
+    td = []
+    for r in range(reps + 1):
+        rows.copy_(bad)
+        be.sync()
+        t0 = time.perf_counter()
+        h.decode_batch_device(b, N, b + k, N, k, n, ok.data_ptr(), cor.data_ptr(), stream=s)
+        be.sync()
+        if r:
+            td.append(time.perf_counter() - t0)
+    nbad = be.n_bad((ok, cor), nerr) + be.n_diff(rows, clean)
+    idx = sample_index(n)
+    o = Oracle(*params)
+    smp_clean, smp_bad = be.host(clean, idx), be.host(bad, idx)
+    mism = int((o.encode_batch(smp_clean[:, :k]) != smp_clean[:, k:]).any(1).sum())
+    ook, ocor, od, op = o.decode_batch(smp_bad[:, :k], smp_bad[:, k:])
+    got = be.host(rows, idx)
+    gok, gcor = be.host(ok, idx), be.host(cor, idx)
+    mism += int(((ook != gok) | (ocor != gcor) | (od != got[:, :k]).any(1) | (op != got[:, k:]).any(1)).sum())
+    e, d = float(np.median(te)), float(np.median(td))
+    h.close()
+    return {"code": f"RS(255,{k}): symbol_size {m}, poly {poly:#x}, fcr {fcr}, prim {prim}, {nr} roots",
+            "kernels": "rs_generic.hip (rsg_encode_k, rsg_decode_k)", "codewords": n, "errors_per_codeword": nerr,
+            "encode_cw_per_s": round(n / e, 1), "decode_cw_per_s": round(n / d, 1),
+            "encode_ms": round(e * 1e3, 4), "decode_ms": round(d * 1e3, 4),
+            "hbm_frac_encode": round(n * N / e / 1e9 / HBM_PEAK_GBS, 4),
+            "hbm_frac_decode": round(n * N / d / 1e9 / HBM_PEAK_GBS, 4),
+            "timing": f"wall time per call, stream-synchronised, median of {reps}",
+            "verified": nbad == 0 and mism == 0,
+            "sample": {"checker": "port: oracle/rs_oracle.c (pinned)", "n": int(len(idx)), "mismatches": mism}}
+
+
 def call_latency(be, calls=2000):
     """The reference's calling pattern: one codeword per poporon_encode /
     poporon_decode call (include/poporon.h:90-91), host buffers, on the GPU
@@ -1159,6 +1223,10 @@ def main(argv=None):
             line["host_pipeline"] = hp
         if world == 1 and not args.no_latency:
             line["single_call_latency"] = call_latency(be)
+        if world == 1 and not args.no_general:
+            gp = general_params(be)
+            line["general_params"] = gp
+            line["verified"] = line["verified"] and gp["verified"]
     else:
         if "decode_mixed" in line:
             line["decode_mixed"].pop("_kt", None)
