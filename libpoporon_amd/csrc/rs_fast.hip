@@ -484,9 +484,17 @@ __global__ __launch_bounds__(FWG, 8) void rs_chien_k(const RsDevTables *__restri
  * The locations and magnitudes go out as a 32-byte record per codeword for
  * rs_apply_k.
  */
+#ifndef F2WG
 #define F2WG 768 /* a multiple of four waves: 640-thread groups leave SIMDs uneven (0.084 ms) */
+#endif
+#ifndef F2_WAVES
+#define F2_WAVES (F2WG / 128)
+#endif
+#ifndef FORNEY_R
+#define FORNEY_R 4 /* roots per step */
+#endif
 template <bool P11>
-__global__ __launch_bounds__(F2WG, 6) void rs_forney_k(const RsDevTables *__restrict__ T, RsCorrParams P,
+__global__ __launch_bounds__(F2WG, F2_WAVES) void rs_forney_k(const RsDevTables *__restrict__ T, RsCorrParams P,
                                                       uint8_t *data, size_t dstride, uint8_t *parity, size_t pstride,
                                                       size_t count, const uint8_t *__restrict__ lam,
                                                       const uint8_t *__restrict__ om, uint8_t *__restrict__ roots,
@@ -499,7 +507,7 @@ __global__ __launch_bounds__(F2WG, 6) void rs_forney_k(const RsDevTables *__rest
     const GfA gf{lds_addr(lgf) + 4u * (threadIdx.x & 31u) + 1u};
     const int32_t pad = P.pad;
     constexpr bool fcr1 = P11, iprim1 = P11;
-    constexpr int R = 4;
+    constexpr int R = FORNEY_R;
     const uint32_t mp = 255u * 128u + gf.pofs; /* alpha^(log a - log b) = expa(loga a - loga b + mp) */
 
     for (size_t base = (size_t)blockIdx.x * F2WG; base < count; base += (size_t)gridDim.x * F2WG) {
