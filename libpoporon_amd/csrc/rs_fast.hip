@@ -478,20 +478,24 @@ __global__ __launch_bounds__(FWG, 8) void rs_chien_k(const RsDevTables *__restri
  * log den) (no den = 0 guard, as the reference); a zero numerator corrects
  * nothing and is not counted.  The sums split at m = 8: one 8-step power
  * chain per root serves Omega_0..7 / Omega_8..15 and the derivative's lower
- * / upper four terms, merged by alpha^(8i); four roots per step, the logs
- * unpacked (80 VGPRs, 6 waves/SIMD in 768-thread groups: 0.062 -> 0.059 ms
- * against the even/odd chains at 8 waves, profiles/r03_forney_split8.log).
+ * / upper four terms, merged by alpha^(8i) (0.062 -> 0.059 ms against the
+ * even/odd chains, profiles/r03_forney_split8.log); FORNEY_R roots per step
+ * (below), the logs unpacked.
  * The locations and magnitudes go out as a 32-byte record per codeword for
  * rs_apply_k.
  */
+/* rs_forney_k: two roots per step at 62 VGPRs, 8 waves/SIMD in 1024-thread
+ * groups: 0.0501-0.0508 vs 0.0519-0.0535 ms for four roots per step at 79
+ * VGPRs, 6 waves in 768-thread groups (profiles/r05_forney_r2_ab.log; a
+ * 640-thread group leaves SIMDs uneven: 0.084 ms) */
 #ifndef F2WG
-#define F2WG 768 /* a multiple of four waves: 640-thread groups leave SIMDs uneven (0.084 ms) */
+#define F2WG 1024
 #endif
 #ifndef F2_WAVES
 #define F2_WAVES (F2WG / 128)
 #endif
 #ifndef FORNEY_R
-#define FORNEY_R 4 /* roots per step */
+#define FORNEY_R 2 /* roots per step */
 #endif
 template <bool P11>
 __global__ __launch_bounds__(F2WG, F2_WAVES) void rs_forney_k(const RsDevTables *__restrict__ T, RsCorrParams P,
