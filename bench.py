@@ -879,11 +879,11 @@ def host_pipeline(be, w, reps=3):
 
 
 def general_params(be, n=1 << 20, reps=5, params=(8, 0x11D, 1, 1, 16), nerr=8):
-    """SURVEY 8(f) row 1, the general-parameter kernels (rs_generic.hip: one
-    codeword per lane, per-lane arrays in LDS): RS(255, 239) -- the default
-    field with 16 roots, which the RS(255,223) kernels do not serve -- encode of
-    n resident messages and decode with t = 8 random errors per codeword, wall
-    time per call (stream-synchronised, median of reps).  Every 4096th codeword
+    """SURVEY 8(f) row 1, general parameters: RS(255, 239) -- the default field
+    with 16 roots -- encode of n resident messages (the RS(255,223) LFSR kernel
+    run with g(x) x^16, rsk_encode_nr) and decode with t = 8 random errors per
+    codeword (rs_generic.hip: one codeword per lane, per-lane arrays in LDS),
+    wall time per call (stream-synchronised, median of reps).  Every 4096th codeword
     is compared with the oracle restatement (oracle/rs_oracle.c, pinned to the
     compiled reference's golden vectors for 13 parameter sets)."""
     import numpy as np
@@ -931,7 +931,8 @@ def general_params(be, n=1 << 20, reps=5, params=(8, 0x11D, 1, 1, 16), nerr=8):
     e, d = float(np.median(te)), float(np.median(td))
     h.close()
     return {"code": f"RS(255,{k}): symbol_size {m}, poly {poly:#x}, fcr {fcr}, prim {prim}, {nr} roots",
-            "kernels": "rs_generic.hip (rsg_encode_k, rsg_decode_k)", "codewords": n, "errors_per_codeword": nerr,
+            "kernels": "encode: rs_lfsr_k<ENCODE> with g(x) x^(32 - nr) (rsk_encode_nr); decode: rs_generic.hip "
+                       "(rsg_decode_k)", "codewords": n, "errors_per_codeword": nerr,
             "encode_cw_per_s": round(n / e, 1), "decode_cw_per_s": round(n / d, 1),
             "encode_ms": round(e * 1e3, 4), "decode_ms": round(d * 1e3, 4),
             "hbm_frac_encode": round(n * N / e / 1e9 / HBM_PEAK_GBS, 4),

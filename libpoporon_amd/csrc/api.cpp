@@ -174,6 +174,7 @@ struct _poporon_t {
     int decode_path; /* 0: by batch size, 1: split kernels (rs_fast.hip), 2: single kernel (rs_correct_k),
                       * 3: one codeword per wave (rs_wave_k) */
     bool generic;   /* served by the general-parameter kernels (rs_generic.hip) */
+    bool lfsr_nr;   /* generic byte-symbol code, num_roots < 32: batch encodes on the LFSR kernel (rsk_encode_nr) */
     RsDevTables host_tab;
     RsCorrParams corr;
     RsGenTables gen_tab;
@@ -574,6 +575,48 @@ static bool params_supported(const poporon_t *h)
     return true;
 }
 
+/* Byte-symbol codes with fewer than 32 roots encode on the RS(255,223) LFSR
+ * kernel with g'(x) = g(x) x^(32 - nr) (rsk_encode_nr, rs_kernels.hip): the
+ * same steps as src/encode.c:120-143 on the first nr register bytes, zeros
+ * behind them.  Like the fast path it needs a generator without zero
+ * coefficients (the reference's log-form LFSR reads a zero coefficient's log
+ * literally). */
+static bool params_lfsr_nr(const poporon_t *h)
+{
+    const poporon_rs_t *rs = h->rs;
+    if (rs->gf->symbol_size != 8 || rs->num_roots == 0 || rs->num_roots >= RS_NR || rs->primitive_element == 0)
+        return false;
+    for (uint32_t i = 0; i < rs->num_roots; i++)
+        if (rs->generator_polynomial[i] == rs->gf->field_size)
+            return false;
+    return true;
+}
+
+/* rows of g'(x) = g(x) x^(32 - nr) in the LFSR kernel's interleaved layout:
+ * row byte m = fb * g_(nr-1-m) for m < nr (src/encode.c:126-140), 0 past it */
+static void build_lfsr_rows(poporon_t *h)
+{
+    const poporon_rs_t *rs = h->rs;
+    const poporon_gf_t *gf = rs->gf;
+    const uint16_t *g = rs->generator_polynomial;
+    const uint32_t nr = rs->num_roots;
+    RsDevTables &t = h->host_tab;
+    memset(&t, 0, sizeof(t));
+    uint8_t row[32];
+    for (uint32_t fb = 0; fb < 256; fb++) {
+        for (uint32_t m = 0; m < 32; m++)
+            row[m] = (fb == 0 || m >= nr)
+                         ? 0
+                         : (uint8_t)gf->log2exp[gf_mod(gf, (uint16_t)(gf->exp2log[fb] + g[nr - 1 - m]))];
+        uint32_t il[8];
+        for (uint32_t k = 0; k < 8; k++)
+            il[k] = (uint32_t)row[k] | ((uint32_t)row[k + 8] << 8) | ((uint32_t)row[k + 16] << 16) |
+                    ((uint32_t)row[k + 24] << 24);
+        memcpy(&t.lfsr[fb * 2], il, 16);
+        memcpy(&t.lfsr[fb * 2 + 1], il + 4, 16);
+    }
+}
+
 /* ---- BCH handle: generator from minimal polynomials (src/bch.c:184-285) ---- */
 static uint32_t bch_min_poly(const poporon_gf_t *gf, uint32_t e)
 {
@@ -695,11 +738,14 @@ EXPORT poporon_t *poporon_create(const poporon_config_t *config)
     h->last_corrected = 0;
     h->fast = params_supported(h);
     h->generic = !h->fast && params_generic(h);
+    h->lfsr_nr = h->generic && params_lfsr_nr(h);
     h->supported = h->fast || h->generic;
     if (h->fast)
         build_tables(h);
     if (h->generic)
         build_generic(h);
+    if (h->lfsr_nr)
+        build_lfsr_rows(h);
     return h;
 }
 
@@ -916,6 +962,10 @@ static bool gpu_init_steps(poporon_t *h)
     } else {
         HIP_OK(hipMalloc((void **)&g.gtab, sizeof(RsGenTables)));
         HIP_OK(hipMemcpy(g.gtab, &h->gen_tab, sizeof(RsGenTables), hipMemcpyHostToDevice));
+        if (h->lfsr_nr) { /* the LFSR rows of g(x) x^(32 - nr) (only tab->lfsr is read) */
+            HIP_OK(hipMalloc((void **)&g.tab, sizeof(RsDevTables)));
+            HIP_OK(hipMemcpy(g.tab, &h->host_tab, sizeof(RsDevTables), hipMemcpyHostToDevice));
+        }
     }
     g.ready = true;
     return true;
@@ -1151,6 +1201,9 @@ static bool launch_encode(poporon_t *h, const uint8_t *d_data, size_t ds, uint8_
         HIP_OK(rsk_encode1(h->gpu.tab, d_data, d_par, (uint32_t)size, nullptr, 0, s));
     } else if (h->fast) {
         HIP_OK(rsk_encode(h->gpu.tab, d_data, ds, d_par, ps, (uint32_t)size, count, h->gpu.num_cu, s));
+    } else if (h->lfsr_nr && count > 1) {
+        HIP_OK(rsk_encode_nr(h->gpu.tab, d_data, ds, d_par, ps, (uint32_t)size, count, h->rs->num_roots,
+                             h->gpu.num_cu, s));
     } else {
         RsGenParams prm = h->gen;
         prm.size = (uint32_t)size;

@@ -153,6 +153,11 @@ extern "C" {
 hipError_t rsk_encode(const RsDevTables *tab, const uint8_t *data, size_t dstride, uint8_t *parity, size_t pstride,
                       uint32_t size, size_t count, int num_cu, hipStream_t stream);
 
+/* the same LFSR for a byte-symbol code of npar < 32 roots (g(x) x^(32 - npar)
+ * in tab->lfsr): npar parity bytes per codeword */
+hipError_t rsk_encode_nr(const RsDevTables *tab, const uint8_t *data, size_t dstride, uint8_t *parity, size_t pstride,
+                         uint32_t size, size_t count, uint32_t npar, int num_cu, hipStream_t stream);
+
 /* 32 syndromes (poly form, S_i = c(beta_i)) per codeword into syn: the
  * encoder's LFSR over the data, XORed with the received parity (E'), and the
  * synt transform */

@@ -382,8 +382,16 @@ __device__ __forceinline__ void store32_any(uint8_t *o, const uint32_t (&P)[8])
 template <int MODE>
 __device__ __forceinline__ void lfsr_epilogue(const uint32_t (&P)[8], const uint4 *__restrict__ synt, size_t cw,
                                               uint8_t *__restrict__ parity, size_t pstride,
-                                              uint8_t *__restrict__ out)
+                                              uint8_t *__restrict__ out, uint32_t npar = RS_NR)
 {
+    if (MODE == MODE_ENCODE && npar < RS_NR) {
+        /* a generator of degree npar < 32 run as g(x) x^(32 - npar): its
+         * parity is the register's first npar bytes (rsk_encode_nr) */
+        uint8_t *o = parity + cw * pstride;
+        for (uint32_t m = 0; m < npar; ++m)
+            o[m] = (uint8_t)(P[m >> 2] >> (8u * (m & 3u)));
+        return;
+    }
     if (MODE == MODE_SYNDROME) {
         /* S = sum over the bytes m of E' of T_m,lo[e_m & 15] ^ T_m,hi[e_m >> 4] */
         uint32_t S[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -428,7 +436,7 @@ __global__ __launch_bounds__(LFSR_WG) void rs_lfsr_k(const RsDevTables *__restri
                                                       const uint8_t *__restrict__ data, size_t dstride,
                                                       uint8_t *__restrict__ parity, size_t pstride, uint32_t size,
                                                       size_t count, uint8_t *__restrict__ out,
-                                                      uint32_t *__restrict__ reset)
+                                                      uint32_t *__restrict__ reset, uint32_t npar)
 {
     if (reset && blockIdx.x == 0 && threadIdx.x == 0) {
         reset[0] = 0u; /* the split decode's list length, before any later launch on the stream */
@@ -465,7 +473,7 @@ __global__ __launch_bounds__(LFSR_WG) void rs_lfsr_k(const RsDevTables *__restri
                 for (int q = 0; q < 8; ++q)
                     P[q] ^= Q[q];
             }
-            lfsr_epilogue<MODE>(P, synt, cw, parity, pstride, out);
+            lfsr_epilogue<MODE>(P, synt, cw, parity, pstride, out, npar);
         }
     } else if (PATH == PATH_CONTIG && MODE != MODE_ENCODE) {
         /* data || parity as one 255-byte stream */
@@ -547,21 +555,21 @@ static int persistent_grid(size_t count, int wg, int num_cu) /* one round: 2 and
 template <int MODE>
 static hipError_t launch_lfsr(const RsDevTables *tab, const uint8_t *data, size_t dstride, const uint8_t *parity,
                               size_t pstride, uint32_t size, size_t count, uint8_t *out, int num_cu,
-                              hipStream_t stream, uint32_t *reset = nullptr)
+                              hipStream_t stream, uint32_t *reset = nullptr, uint32_t npar = RS_NR)
 {
     if (count == 0)
         return hipSuccess;
     const dim3 grid(persistent_grid(count, LFSR_WG, num_cu)), block(LFSR_WG);
     uint8_t *par = const_cast<uint8_t *>(parity);
-    if (size != FULL_K)
+    if (size != FULL_K || npar != RS_NR)
         RS_LAUNCH((rs_lfsr_k<MODE, PATH_GENERIC>), grid, block, 0, stream, tab, data, dstride, par, pstride,
-                           size, count, out, reset);
+                           size, count, out, reset, npar);
     else if (MODE != MODE_ENCODE && parity == data + FULL_K && pstride == dstride)
         RS_LAUNCH((rs_lfsr_k<MODE, PATH_CONTIG>), grid, block, 0, stream, tab, data, dstride, par, pstride,
-                           size, count, out, reset);
+                           size, count, out, reset, npar);
     else
         RS_LAUNCH((rs_lfsr_k<MODE, PATH_SPLIT>), grid, block, 0, stream, tab, data, dstride, par, pstride,
-                           size, count, out, reset);
+                           size, count, out, reset, npar);
     return hipGetLastError();
 }
 
@@ -569,6 +577,19 @@ extern "C" hipError_t rsk_encode(const RsDevTables *tab, const uint8_t *data, si
                                  size_t pstride, uint32_t size, size_t count, int num_cu, hipStream_t stream)
 {
     return launch_lfsr<MODE_ENCODE>(tab, data, dstride, parity, pstride, size, count, nullptr, num_cu, stream);
+}
+
+/* Byte-symbol codes with npar < 32 roots (the general-parameter handles):
+ * the same LFSR with g'(x) = g(x) x^(32 - npar), whose rows the host builds
+ * with zeros in the low 32 - npar bytes (api.cpp build_lfsr_rows):
+ * m(x) x^32 mod g' = (m(x) x^npar mod g) x^(32 - npar), so the register's
+ * first npar bytes are the parity, highest degree first, the rest stay 0. */
+extern "C" hipError_t rsk_encode_nr(const RsDevTables *tab, const uint8_t *data, size_t dstride, uint8_t *parity,
+                                    size_t pstride, uint32_t size, size_t count, uint32_t npar, int num_cu,
+                                    hipStream_t stream)
+{
+    return launch_lfsr<MODE_ENCODE>(tab, data, dstride, parity, pstride, size, count, nullptr, num_cu, stream, nullptr,
+                                    npar);
 }
 
 extern "C" hipError_t rsk_syndrome(const RsDevTables *tab, const uint8_t *data, size_t dstride, const uint8_t *parity,
