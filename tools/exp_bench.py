@@ -22,7 +22,7 @@ for lib in sys.argv[1:]:
         print(os.path.basename(lib), "FAILED", r.stderr[-400:], flush=True)
         continue
     d = json.loads(line[-1])
-    out = {"value": d["value"], "encode": d["roofline_modes"]["encode"]["kernels_ms"],
+    out = {"value": d["value"], "verified": d.get("verified"), "encode": d["roofline_modes"]["encode"]["kernels_ms"],
            "decode16": d["roofline_modes"]["decode16"]["kernels_ms"]}
     for k in ("erasure_decode_32", "errata_decode_16e8"):
         out[k] = {"cw_per_s": d[k]["cw_per_s"], "ms": d[k]["kernels_avg_ms"]}
