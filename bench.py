@@ -882,7 +882,8 @@ def general_params(be, n=1 << 20, reps=5, params=(8, 0x11D, 1, 1, 16), nerr=8):
     """SURVEY 8(f) row 1, general parameters: RS(255, 239) -- the default field
     with 16 roots -- encode of n resident messages (the RS(255,223) LFSR kernel
     run with g(x) x^16, rsk_encode_nr) and decode with t = 8 random errors per
-    codeword (rs_generic.hip: one codeword per lane, per-lane arrays in LDS),
+    codeword (the split kernels with npar = 16: rsk_syndrome_reset_nr,
+    rs_bm_k<true>, Chien, Forney, rsk_apply_nr; the list on rs_generic.hip),
     wall time per call (stream-synchronised, median of reps).  Every 4096th codeword
     is compared with the oracle restatement (oracle/rs_oracle.c, pinned to the
     compiled reference's golden vectors for 13 parameter sets)."""
@@ -931,8 +932,9 @@ def general_params(be, n=1 << 20, reps=5, params=(8, 0x11D, 1, 1, 16), nerr=8):
     e, d = float(np.median(te)), float(np.median(td))
     h.close()
     return {"code": f"RS(255,{k}): symbol_size {m}, poly {poly:#x}, fcr {fcr}, prim {prim}, {nr} roots",
-            "kernels": "encode: rs_lfsr_k<ENCODE> with g(x) x^(32 - nr) (rsk_encode_nr); decode: rs_generic.hip "
-                       "(rsg_decode_k)", "codewords": n, "errors_per_codeword": nerr,
+            "kernels": "encode: rs_lfsr_k<ENCODE> with g(x) x^(32 - nr) (rsk_encode_nr); decode: the split "
+                       "kernels with npar = nr (rsk_syndrome_reset_nr, rs_bm_k<true>, rs_chien_k, rs_forney_k, "
+                       "rsk_apply_nr; hand-off list on rsg_decode_k)", "codewords": n, "errors_per_codeword": nerr,
             "encode_cw_per_s": round(n / e, 1), "decode_cw_per_s": round(n / d, 1),
             "encode_ms": round(e * 1e3, 4), "decode_ms": round(d * 1e3, 4),
             "hbm_frac_encode": round(n * N / e / 1e9 / HBM_PEAK_GBS, 4),

@@ -175,6 +175,7 @@ struct _poporon_t {
                       * 3: one codeword per wave (rs_wave_k) */
     bool generic;   /* served by the general-parameter kernels (rs_generic.hip) */
     bool lfsr_nr;   /* generic byte-symbol code, num_roots < 32: batch encodes on the LFSR kernel (rsk_encode_nr) */
+    bool nrsplit;   /* ... and large error-mode batches decode on the split kernels (params_nrsplit) */
     RsDevTables host_tab;
     RsCorrParams corr;
     RsGenTables gen_tab;
@@ -430,6 +431,8 @@ EXPORT void poporon_config_destroy(poporon_config_t *config) { free(config); }
 /* handle                                                                   */
 /* ------------------------------------------------------------------------ */
 
+static void build_decode_tables(poporon_t *h, uint32_t nr);
+
 /* Kernel tables for the handle (see rs_device.h for their definitions). */
 static void build_tables(poporon_t *h)
 {
@@ -466,6 +469,19 @@ static void build_tables(poporon_t *h)
             }
         }
     }
+    build_decode_tables(h, RS_NR);
+}
+
+/* Everything but the LFSR rows and encq, for a code of nr <= 32 roots: GF
+ * tables, decode parameters, E' -> syndrome nibble tables, Chien rows, the
+ * split kernels' GF image.  For nr < 32, E' sits in the first nr register
+ * bytes (byte m = coefficient of x^(nr-1-m), zeros behind) and the tables
+ * give S_0..S_(nr-1), zeros behind them. */
+static void build_decode_tables(poporon_t *h, uint32_t nr)
+{
+    const poporon_rs_t *rs = h->rs;
+    const poporon_gf_t *gf = rs->gf;
+    RsDevTables &t = h->host_tab;
     for (uint32_t x = 0; x < 512; x++)
         t.exp2[x] = (uint8_t)gf->log2exp[x % 255];
     t.exp2[511] = 0; /* ZLOG sentinel of the correction kernel (no sum of two logs reaches 511) */
@@ -477,7 +493,7 @@ static void build_tables(poporon_t *h)
     p.fcr = rs->first_consecutive_root;
     p.prim = rs->primitive_element;
     p.iprim = h->primitive_inverse;
-    p.vfast = ((uint64_t)(p.fcr + RS_NR - 1) * p.prim * 254u) < 32768u;
+    p.vfast = ((uint64_t)(p.fcr + nr - 1) * p.prim * 254u) < 32768u;
 
     /* E' -> syndrome nibble tables (rs_device.h) */
     auto gmul = [&](uint32_t x, uint32_t logc) -> uint8_t {
@@ -488,7 +504,11 @@ static void build_tables(poporon_t *h)
             for (uint32_t v = 0; v < 16; v++) {
                 uint8_t rowb[RS_NR];
                 for (uint32_t i = 0; i < RS_NR; i++) {
-                    const uint64_t e = (uint64_t)(RS_NR - 1 - m) * p.prim * (p.fcr + i);
+                    if (m >= nr || i >= nr) {
+                        rowb[i] = 0;
+                        continue;
+                    }
+                    const uint64_t e = (uint64_t)(nr - 1 - m) * p.prim * (p.fcr + i);
                     rowb[i] = gmul(v << (4 * n), (uint32_t)(e % 255));
                 }
                 memcpy(&t.synt[((m * 2 + n) * 2 + 0) * 16 + v], rowb, 16);
@@ -590,6 +610,22 @@ static bool params_lfsr_nr(const poporon_t *h)
         if (rs->generator_polynomial[i] == rs->gf->field_size)
             return false;
     return true;
+}
+
+/* Byte-symbol codes with 2 <= nr < 32 roots decode large error-mode batches
+ * on the split kernels (rsk_syndrome_reset_nr .. rsk_apply_nr, the list on
+ * the general kernel): the LFSR conditions above, distinct roots (prim
+ * coprime to 255: "remainder zero" <=> "all syndromes zero") and the fast
+ * path's exponent bound, as params_supported. */
+static bool params_nrsplit(const poporon_t *h)
+{
+    const poporon_rs_t *rs = h->rs;
+    if (!params_lfsr_nr(h) || rs->num_roots < 2)
+        return false;
+    const uint32_t p = rs->primitive_element;
+    if (p % 3 == 0 || p % 5 == 0 || p % 17 == 0)
+        return false;
+    return ((uint32_t)rs->first_consecutive_root + rs->num_roots - 1) * p + 254u < 65536u;
 }
 
 /* rows of g'(x) = g(x) x^(32 - nr) in the LFSR kernel's interleaved layout:
@@ -739,6 +775,7 @@ EXPORT poporon_t *poporon_create(const poporon_config_t *config)
     h->fast = params_supported(h);
     h->generic = !h->fast && params_generic(h);
     h->lfsr_nr = h->generic && params_lfsr_nr(h);
+    h->nrsplit = h->lfsr_nr && params_nrsplit(h);
     h->supported = h->fast || h->generic;
     if (h->fast)
         build_tables(h);
@@ -746,6 +783,8 @@ EXPORT poporon_t *poporon_create(const poporon_config_t *config)
         build_generic(h);
     if (h->lfsr_nr)
         build_lfsr_rows(h);
+    if (h->nrsplit)
+        build_decode_tables(h, rs->num_roots);
     return h;
 }
 
@@ -962,7 +1001,7 @@ static bool gpu_init_steps(poporon_t *h)
     } else {
         HIP_OK(hipMalloc((void **)&g.gtab, sizeof(RsGenTables)));
         HIP_OK(hipMemcpy(g.gtab, &h->gen_tab, sizeof(RsGenTables), hipMemcpyHostToDevice));
-        if (h->lfsr_nr) { /* the LFSR rows of g(x) x^(32 - nr) (only tab->lfsr is read) */
+        if (h->lfsr_nr) { /* the LFSR rows of g(x) x^(32 - nr) (+ the split decode's tables: nrsplit) */
             HIP_OK(hipMalloc((void **)&g.tab, sizeof(RsDevTables)));
             HIP_OK(hipMemcpy(g.tab, &h->host_tab, sizeof(RsDevTables), hipMemcpyHostToDevice));
         }
@@ -1220,21 +1259,30 @@ static bool launch_encode(poporon_t *h, const uint8_t *d_data, size_t ds, uint8_
  * ~108, 32,768 196 vs ~110 */
 #define SPLIT_MIN_COUNT 16384
 
-/* the split error-mode decode of one sub-batch (rs_fast.hip) */
+/* the split error-mode decode of one sub-batch (rs_fast.hip); npar < 32: a
+ * byte-symbol code of npar roots (h->nrsplit), its list on the general kernel */
 static bool launch_split(poporon_t *h, const RsCorrParams &prm, const RsSplitWs &ws, uint8_t *d_data, size_t ds,
                          uint8_t *d_par, size_t ps, size_t size, size_t count, uint8_t *ok, uint8_t *corrected,
-                         hipStream_t s)
+                         hipStream_t s, uint32_t npar = RS_NR)
 {
     GpuCtx &g = h->gpu;
+    const bool nr = npar < RS_NR;
     {
         KernelTimer t(g, POPORON_AMD_KERNEL_REMAINDER, s);
-        HIP_OK(rsk_syndrome_reset(g.tab, d_data, ds, d_par, ps, (uint32_t)size, count, ws.syn, ws.nlist, g.num_cu,
-                                  s));
+        if (nr)
+            HIP_OK(rsk_syndrome_reset_nr(g.tab, d_data, ds, d_par, ps, (uint32_t)size, count, ws.syn, ws.nlist, npar,
+                                         g.num_cu, s));
+        else
+            HIP_OK(rsk_syndrome_reset(g.tab, d_data, ds, d_par, ps, (uint32_t)size, count, ws.syn, ws.nlist,
+                                      g.num_cu, s));
         t.done();
     }
     {
         KernelTimer t(g, POPORON_AMD_KERNEL_BM, s);
-        HIP_OK(rsk_bm(g.tab, &ws, count, ok, corrected, g.num_cu, s));
+        if (nr)
+            HIP_OK(rsk_bm_nr(g.tab, &ws, count, npar, ok, corrected, g.num_cu, s));
+        else
+            HIP_OK(rsk_bm(g.tab, &ws, count, ok, corrected, g.num_cu, s));
         t.done();
     }
     {
@@ -1249,14 +1297,25 @@ static bool launch_split(poporon_t *h, const RsCorrParams &prm, const RsSplitWs 
     }
     {
         KernelTimer t(g, POPORON_AMD_KERNEL_APPLY, s);
-        HIP_OK(rsk_apply(&prm, &ws, d_data, ds, d_par, ps, count, s));
+        if (nr)
+            HIP_OK(rsk_apply_nr(&prm, &ws, d_data, ds, d_par, ps, count, npar, s));
+        else
+            HIP_OK(rsk_apply(&prm, &ws, d_data, ds, d_par, ps, count, s));
         t.done();
     }
     {
         /* what the split kernels hand on: one codeword per wave (rs_wave_k) */
         KernelTimer t(g, POPORON_AMD_KERNEL_LIST, s);
-        HIP_OK(rsk_wave(g.tab, &prm, d_data, ds, d_par, ps, count, ws.list, ws.nlist, ws.syn, nullptr, 0, nullptr,
-                        nullptr, 0, nullptr, ok, corrected, g.num_cu, s));
+        if (nr) {
+            RsGenParams gp = h->gen;
+            gp.size = (uint32_t)size;
+            gp.pad = prm.pad;
+            HIP_OK(rsg_decode_list(g.gtab, &gp, d_data, ds, d_par, ps, count, ws.list, ws.nlist, ok, corrected,
+                                   g.num_cu, s));
+        } else {
+            HIP_OK(rsk_wave(g.tab, &prm, d_data, ds, d_par, ps, count, ws.list, ws.nlist, ws.syn, nullptr, 0, nullptr,
+                            nullptr, 0, nullptr, ok, corrected, g.num_cu, s));
+        }
         t.done();
     }
     return true;
@@ -1276,6 +1335,25 @@ static bool launch_decode(poporon_t *h, uint8_t *d_data, size_t ds, uint8_t *d_p
         HIP_OK(bchk_decode(&h->bch, d_data, ds, d_par, ps, count, ok, corrected, h->gpu.num_cu, s));
         t.done();
         return true;
+    }
+    if (h->nrsplit && !ext_syn && !pos8 && !pos32 && h->corr.vfast && !h->corr.force_verify &&
+        (h->decode_path == 1 || (h->decode_path == 0 && count >= SPLIT_MIN_COUNT))) {
+        /* a byte-symbol code of fewer than 32 roots, errors only: the split
+         * kernels with npar = num_roots, the list on the general kernel */
+        RsCorrParams prm = h->corr;
+        prm.size = (uint32_t)size;
+        prm.pad = (int32_t)(h->rs->gf->field_size - h->rs->num_roots - size);
+        const bool shared = !rem;
+        if (shared) {
+            if (!ensure_rem(h, count) || !rem_acquire(h->gpu, s))
+                return false;
+            rem = h->gpu.rem;
+            rem_cap = h->gpu.rem_cap;
+        }
+        const RsSplitWs ws = rs_ws_carve(rem, rem_cap ? rem_cap : count);
+        if (!launch_split(h, prm, ws, d_data, ds, d_par, ps, size, count, ok, corrected, s, h->rs->num_roots))
+            return false;
+        return !shared || rem_release(h->gpu, s);
     }
     if (!h->fast) {
         RsGenParams prm = h->gen;

@@ -275,6 +275,23 @@ hipError_t rsk_apply(const RsCorrParams *prm, const RsSplitWs *ws, uint8_t *data
                      size_t pstride, size_t count, hipStream_t stream);
 
 /*
+ * The same split decode for a byte-symbol code of npar < 32 roots (tab from
+ * api.cpp build_tables_nr; RsCorrParams.pad = 255 - npar - size):
+ *   rsk_syndrome_reset_nr  npar syndromes (zeros behind them) into ws.syn
+ *   rsk_bm_nr              npar BM iterations; fast only while 2L <= npar
+ *   rsk_chien, rsk_forney  unchanged (they depend on pad, fcr and prim only)
+ *   rsk_apply_nr           positions below size + npar
+ * then the general-parameter kernel over ws.list (rsg_decode_list).
+ */
+hipError_t rsk_syndrome_reset_nr(const RsDevTables *tab, const uint8_t *data, size_t dstride, const uint8_t *parity,
+                                 size_t pstride, uint32_t size, size_t count, uint8_t *syn, uint32_t *reset,
+                                 uint32_t npar, int num_cu, hipStream_t stream);
+hipError_t rsk_bm_nr(const RsDevTables *tab, const RsSplitWs *ws, size_t count, uint32_t npar, uint8_t *ok,
+                     uint8_t *corrected, int num_cu, hipStream_t stream);
+hipError_t rsk_apply_nr(const RsCorrParams *prm, const RsSplitWs *ws, uint8_t *data, size_t dstride, uint8_t *parity,
+                        size_t pstride, size_t count, uint32_t npar, hipStream_t stream);
+
+/*
  * Split erasure-mode decode, after rsk_syndrome into ws.syn:
  *   rsk_correct_era_rec  the general kernel's erasure decode with the
  *                        corrections written as 64-byte records (32 slot

@@ -91,11 +91,16 @@ static int fast_grid(size_t count, int num_cu)
  * 4-lookup log form at 8 waves/SIMD; the same at 8, 6 or 5 waves spilled
  * (profiles/r03_bm_value.log).
  */
+/* NRG: a byte-symbol code of npar < 32 roots (syndromes S_0..S_(npar-1),
+ * zeros behind them): npar iterations, and the fast path needs 2L <= npar
+ * besides -- the bound under which the locator's roots and Forney's
+ * magnitudes reproduce every syndrome -- the rest goes to the list */
+template <bool NRG>
 __global__ __launch_bounds__(BWG, BM_WAVES) void rs_bm_k(const RsDevTables *__restrict__ T, const uint8_t *__restrict__ syn,
                                                    size_t count, uint8_t *__restrict__ lamo, uint8_t *__restrict__ omo,
                                                    uint8_t *__restrict__ meta, uint32_t *__restrict__ list,
                                                    uint32_t *__restrict__ nlist, uint8_t *__restrict__ ok,
-                                                   uint8_t *__restrict__ corrected)
+                                                   uint8_t *__restrict__ corrected, uint32_t npar)
 {
     __shared__ uint32_t lgf[512 * 32];
     fill_gfa<BWG>(lgf, T);
@@ -222,10 +227,11 @@ __global__ __launch_bounds__(BWG, BM_WAVES) void rs_bm_k(const RsDevTables *__re
                 lb = ld;
             }
         };
+        const uint32_t nq = NRG ? (npar + 3u) >> 2 : RS_NR / 4;
 #pragma unroll 1
-        for (uint32_t q = 0; q < RS_NR / 4; ++q) {
+        for (uint32_t q = 0; q < nq; ++q) {
             const uint32_t sd = snext;
-            if (q + 1u < RS_NR / 4) /* uniform */
+            if (q + 1u < nq) /* uniform */
                 snext = any ? sp[q + 1u] : 0u;
             /* shift the window by four entries, S_(4q+3) .. S_(4q) in front */
             const uint32_t s0 = gf.logs(sd & 0xffu), s1 = gf.logs((sd >> 8) & 0xffu);
@@ -235,9 +241,12 @@ __global__ __launch_bounds__(BWG, BM_WAVES) void rs_bm_k(const RsDevTables *__re
                 WL[k] = WL[k - 4];
             WL[0] = s3, WL[1] = s2, WL[2] = s1, WL[3] = s0;
             step(std::integral_constant<int, 0>{}, 4u * q + 1u);
-            step(std::integral_constant<int, 1>{}, 4u * q + 2u);
-            step(std::integral_constant<int, 2>{}, 4u * q + 3u);
-            step(std::integral_constant<int, 3>{}, 4u * q + 4u);
+            if (!NRG || 4u * q + 2u <= npar) /* uniform */
+                step(std::integral_constant<int, 1>{}, 4u * q + 2u);
+            if (!NRG || 4u * q + 3u <= npar)
+                step(std::integral_constant<int, 2>{}, 4u * q + 3u);
+            if (!NRG || 4u * q + 4u <= npar)
+                step(std::integral_constant<int, 3>{}, 4u * q + 4u);
         }
 
         uint32_t al[NL]; /* address-form logs of the final Lambda */
@@ -250,7 +259,7 @@ __global__ __launch_bounds__(BWG, BM_WAVES) void rs_bm_k(const RsDevTables *__re
 #pragma unroll
         for (int i = 0; i < NL; ++i)
             deg = (al[i] & 1u) ? (uint32_t)i : deg;
-        const bool fast = any && !over && deg == L && deg != 0u;
+        const bool fast = any && !over && deg == L && deg != 0u && (!NRG || 2u * L <= npar);
 
         /* ---- Omega = S * Lambda mod x^deg (log form), src/decode.c:147-158 ---- */
         uint32_t ob[4] = {0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
@@ -830,7 +839,7 @@ __global__ __launch_bounds__(BPWG, BP_WAVES) void rs_era_bp_k(const RsDevTables 
 template <int NC> /* corrections per record: 16 (error mode) or 32 (erasure mode) */
 __global__ __launch_bounds__(AWG) void rs_apply_k(const uint8_t *__restrict__ meta, const uint8_t *__restrict__ rec,
                                                   uint8_t *data, size_t dstride, uint8_t *parity, size_t pstride,
-                                                  uint32_t size, size_t count, uint32_t wire)
+                                                  uint32_t size, size_t count, uint32_t wire, uint32_t npar)
 {
     constexpr int NW = NC / 4; /* record dwords of positions (then as many of magnitudes) */
     __shared__ uint4 img[AWG / 64][ABLK];
@@ -858,7 +867,7 @@ __global__ __launch_bounds__(AWG) void rs_apply_k(const uint8_t *__restrict__ me
     if (__ballot(fast) == 0ull)
         return;
     /* positions past the codeword (erasure slots, clamped to 255) are never written */
-    const uint32_t lim = size + RS_NR;
+    const uint32_t lim = size + npar;
     if (wire && base + 64u <= count) { /* uniform */
         const uint4 *src = reinterpret_cast<const uint4 *>(data + base * 255u);
         uint4 *dst = reinterpret_cast<uint4 *>(data + base * 255u);
@@ -920,9 +929,20 @@ extern "C" hipError_t rsk_bm(const RsDevTables *tab, const RsSplitWs *ws, size_t
         return hipSuccess;
     const size_t need = (count + BWG - 1) / BWG,
                  res = FAST_ROUNDS * (size_t)(num_cu > 0 ? num_cu : 256) * (BM_WAVES * 256 / BWG);
-    RS_LAUNCH(rs_bm_k, dim3((uint32_t)(need < res ? need : res)), dim3(BWG), 0, stream, tab, ws->syn, count,
-                       ws->lam,
-                       ws->om, ws->meta, ws->list, ws->nlist, ok, corrected);
+    RS_LAUNCH(rs_bm_k<false>, dim3((uint32_t)(need < res ? need : res)), dim3(BWG), 0, stream, tab, ws->syn, count,
+              ws->lam, ws->om, ws->meta, ws->list, ws->nlist, ok, corrected, (uint32_t)RS_NR);
+    return hipGetLastError();
+}
+
+extern "C" hipError_t rsk_bm_nr(const RsDevTables *tab, const RsSplitWs *ws, size_t count, uint32_t npar, uint8_t *ok,
+                                uint8_t *corrected, int num_cu, hipStream_t stream)
+{
+    if (count == 0)
+        return hipSuccess;
+    const size_t need = (count + BWG - 1) / BWG,
+                 res = FAST_ROUNDS * (size_t)(num_cu > 0 ? num_cu : 256) * (BM_WAVES * 256 / BWG);
+    RS_LAUNCH(rs_bm_k<true>, dim3((uint32_t)(need < res ? need : res)), dim3(BWG), 0, stream, tab, ws->syn, count,
+              ws->lam, ws->om, ws->meta, ws->list, ws->nlist, ok, corrected, npar);
     return hipGetLastError();
 }
 
@@ -953,17 +973,20 @@ extern "C" hipError_t rsk_forney(const RsDevTables *tab, const RsCorrParams *prm
     return hipGetLastError();
 }
 
+/* wire: 255-byte rows back to back (size + npar = 255, parity right after
+ * the data), 16-byte aligned */
 template <int NC>
 static hipError_t apply_launch(const RsCorrParams *prm, const uint8_t *meta, const uint8_t *rec, uint8_t *data,
-                               size_t dstride, uint8_t *parity, size_t pstride, size_t count, hipStream_t stream)
+                               size_t dstride, uint8_t *parity, size_t pstride, size_t count, hipStream_t stream,
+                               uint32_t npar = RS_NR)
 {
     if (count == 0)
         return hipSuccess;
-    const uint32_t wire = prm->size == 223u && dstride == 255u && pstride == 255u && parity == data + 223 &&
-                          (reinterpret_cast<uintptr_t>(data) & 15u) == 0u;
+    const uint32_t wire = prm->size + npar == 255u && dstride == 255u && pstride == 255u &&
+                          parity == data + prm->size && (reinterpret_cast<uintptr_t>(data) & 15u) == 0u;
     const size_t waves = (count + 63) / 64;
     RS_LAUNCH(rs_apply_k<NC>, dim3((uint32_t)((waves + AWG / 64 - 1) / (AWG / 64))), dim3(AWG), 0, stream,
-                       meta, rec, data, dstride, parity, pstride, prm->size, count, wire);
+                       meta, rec, data, dstride, parity, pstride, prm->size, count, wire, npar);
     return hipGetLastError();
 }
 
@@ -971,6 +994,12 @@ extern "C" hipError_t rsk_apply(const RsCorrParams *prm, const RsSplitWs *ws, ui
                                 uint8_t *parity, size_t pstride, size_t count, hipStream_t stream)
 {
     return apply_launch<16>(prm, ws->meta, ws->roots, data, dstride, parity, pstride, count, stream);
+}
+
+extern "C" hipError_t rsk_apply_nr(const RsCorrParams *prm, const RsSplitWs *ws, uint8_t *data, size_t dstride,
+                                   uint8_t *parity, size_t pstride, size_t count, uint32_t npar, hipStream_t stream)
+{
+    return apply_launch<16>(prm, ws->meta, ws->roots, data, dstride, parity, pstride, count, stream, npar);
 }
 
 extern "C" hipError_t rsk_apply_era(const RsCorrParams *prm, const uint8_t *meta, const uint8_t *rec, uint8_t *data,

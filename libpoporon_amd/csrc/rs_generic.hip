@@ -335,6 +335,8 @@ __device__ bool g_correct(const GShared &s, const GMod &mod, const RsGenParams &
  * ext: external log-form syndromes (nroots u16 per codeword at ext_stride),
  * values > nn refuse the codeword (out-of-table in the reference).
  * pos/cnt: erasure lists (erasure-object mode), counts > nroots refused. */
+/* list != NULL: the codewords list[0 .. *list_n) only (the split decode's
+ * hand-off, rsg_decode_list; length read on the device) */
 template <typename PosT>
 __global__ __launch_bounds__(G_WG_MAX) void rsg_decode_k(const RsGenTables *__restrict__ T, RsGenParams P,
                                                           uint8_t *data, size_t dstride, uint8_t *parity,
@@ -342,15 +344,18 @@ __global__ __launch_bounds__(G_WG_MAX) void rsg_decode_k(const RsGenTables *__re
                                                           const uint16_t *__restrict__ ext, size_t ext_stride,
                                                           const PosT *__restrict__ pos, size_t pos_stride,
                                                           const uint8_t *__restrict__ cntv, uint8_t *__restrict__ ok,
-                                                          uint8_t *__restrict__ corrected)
+                                                          uint8_t *__restrict__ corrected,
+                                                          const uint32_t *__restrict__ list,
+                                                          const uint32_t *__restrict__ list_n)
 {
     extern __shared__ uint8_t smem[];
     const GShared s = g_setup(T, smem);
     const GMod mod{P.nn, P.magic};
     const uint32_t nr = P.nroots, A0 = P.nn;
     const LaneArr S{s.arr(0, nr + 1u) + threadIdx.x, s.wg};
-    for (size_t cw = (size_t)blockIdx.x * blockDim.x + threadIdx.x; cw < count;
-         cw += (size_t)gridDim.x * blockDim.x) {
+    const size_t n = list ? (size_t)*list_n : count;
+    for (size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x; idx < n; idx += (size_t)gridDim.x * blockDim.x) {
+        const size_t cw = list ? (size_t)list[idx] : idx;
         uint8_t *d = data + cw * dstride;
         uint8_t *par = parity + cw * pstride;
         uint32_t fixed = 0;
@@ -452,10 +457,28 @@ extern "C" hipError_t rsg_decode(const RsGenTables *tab, const RsGenParams *prm,
     const dim3 grid = g_grid(count, wg, num_cu, lds);
     if (pos32)
         RS_LAUNCH(rsg_decode_k<uint32_t>, grid, dim3(wg), lds, stream, tab, *prm, data, dstride, parity,
-                           pstride, count, ext, ext_stride, pos32, pos_stride, cnt, ok, corrected);
+                           pstride, count, ext, ext_stride, pos32, pos_stride, cnt, ok, corrected, nullptr, nullptr);
     else
         RS_LAUNCH(rsg_decode_k<uint8_t>, grid, dim3(wg), lds, stream, tab, *prm, data, dstride, parity,
-                           pstride, count, ext, ext_stride, pos8, pos_stride, cnt, ok, corrected);
+                           pstride, count, ext, ext_stride, pos8, pos_stride, cnt, ok, corrected, nullptr, nullptr);
+    return hipGetLastError();
+}
+
+/* errors-only decode of the codewords list[0 .. *list_n) (at most count; the
+ * grid is sized for a list of up to 1/16 of the batch and loops past it) */
+extern "C" hipError_t rsg_decode_list(const RsGenTables *tab, const RsGenParams *prm, uint8_t *data, size_t dstride,
+                                      uint8_t *parity, size_t pstride, size_t count, const uint32_t *list,
+                                      const uint32_t *list_n, uint8_t *ok, uint8_t *corrected, int num_cu,
+                                      hipStream_t stream)
+{
+    if (count == 0)
+        return hipSuccess;
+    uint32_t wg;
+    size_t lds;
+    g_shape(*prm, 7, wg, lds);
+    RS_LAUNCH(rsg_decode_k<uint8_t>, g_grid((count + 15) / 16, wg, num_cu, lds), dim3(wg), lds, stream, tab, *prm,
+              data, dstride, parity, pstride, count, (const uint16_t *)nullptr, (size_t)0, (const uint8_t *)nullptr,
+              (size_t)0, (const uint8_t *)nullptr, ok, corrected, list, list_n);
     return hipGetLastError();
 }
 

@@ -204,6 +204,27 @@ __device__ __forceinline__ void load32_any(uint32_t (&Q)[8], const uint8_t *p)
         Q[k] = __builtin_amdgcn_alignbyte(W[k + 1], W[k], sh);
 }
 
+/* The first n < 32 bytes at p (any alignment) as 8 dwords in order, zeros
+ * behind them: only aligned dwords that hold one of the n bytes are loaded
+ * (the parity of a code with n < 32 roots; the row may end right after it) */
+__device__ __forceinline__ void load_n_any(uint32_t (&Q)[8], const uint8_t *p, uint32_t n)
+{
+    const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+    gu32 *w = reinterpret_cast<gu32 *>(a & ~uintptr_t(3));
+    const uint32_t sh = static_cast<uint32_t>(a & 3u);
+    const uint32_t nd = (sh + n + 3u) >> 2; /* dwords holding the n bytes */
+    uint32_t W[9];
+#pragma unroll
+    for (int k = 0; k < 9; ++k)
+        W[k] = (uint32_t)k < nd ? w[k] : 0u;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        const uint32_t v = __builtin_amdgcn_alignbyte(W[k + 1], W[k], sh);
+        const uint32_t have = n > 4u * k ? n - 4u * k : 0u; /* bytes of dword k inside the n */
+        Q[k] = have >= 4u ? v : v & ((1u << (8u * have)) - 1u);
+    }
+}
+
 /* Where the next codeword's bytes of one stream are: its 16-byte aligned
  * chunks and the offset of the first byte in the first chunk.  With no next
  * codeword for this lane (valid = false) the chunks are read from `fallback`
@@ -468,7 +489,10 @@ __global__ __launch_bounds__(LFSR_WG) void rs_lfsr_k(const RsDevTables *__restri
             il_bytes(P, X, 0);
             if (MODE != MODE_ENCODE) { /* E' = received parity + parity of the received data */
                 uint32_t Q[8];
-                load32_any(Q, parity + cw * pstride);
+                if (npar < RS_NR) /* g(x) x^(32 - npar): E' in the first npar bytes, zeros behind */
+                    load_n_any(Q, parity + cw * pstride, npar);
+                else
+                    load32_any(Q, parity + cw * pstride);
 #pragma unroll
                 for (int q = 0; q < 8; ++q)
                     P[q] ^= Q[q];
@@ -604,6 +628,19 @@ extern "C" hipError_t rsk_syndrome_reset(const RsDevTables *tab, const uint8_t *
                                          uint8_t *syn, uint32_t *reset, int num_cu, hipStream_t stream)
 {
     return launch_lfsr<MODE_SYNDROME>(tab, data, dstride, parity, pstride, size, count, syn, num_cu, stream, reset);
+}
+
+/* the same for a byte-symbol code of npar < 32 roots (tab built by
+ * api.cpp build_tables_nr: LFSR rows of g(x) x^(32 - npar), syndrome tables
+ * S_i = sum_(m < npar) E'_m beta_i^(npar - 1 - m) for i < npar, zero rows
+ * elsewhere): npar syndromes, zeros behind them */
+extern "C" hipError_t rsk_syndrome_reset_nr(const RsDevTables *tab, const uint8_t *data, size_t dstride,
+                                            const uint8_t *parity, size_t pstride, uint32_t size, size_t count,
+                                            uint8_t *syn, uint32_t *reset, uint32_t npar, int num_cu,
+                                            hipStream_t stream)
+{
+    return launch_lfsr<MODE_SYNDROME>(tab, data, dstride, parity, pstride, size, count, syn, num_cu, stream, reset,
+                                      npar);
 }
 
 /* poly-form syndromes (rsk_syndrome's output) -> the reference's log form:

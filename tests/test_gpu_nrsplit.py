@@ -1,0 +1,144 @@
+"""Byte-symbol codes with 2 <= num_roots < 32 on the split decode kernels
+(api.cpp params_nrsplit / launch_split with npar = num_roots): syndromes from
+the LFSR kernel with g(x) x^(32 - nr) (rsk_syndrome_reset_nr), nr BM
+iterations with the fast path bounded by 2L <= nr (rs_bm_k<true>), the
+unchanged Chien and Forney kernels, the block apply over size + nr bytes and
+the general-parameter kernel over the hand-off list (rsg_decode_list).
+
+Every result -- bytes, ok, corrected_num -- is compared with the oracle
+(oracle/rs_oracle.c, pinned to the compiled reference by
+tests/test_oracle_golden.py), over error counts 0 .. t + 3 (past the
+capability too, so the list and the failure paths run), shortened sizes,
+the wire layout (block apply) and strided rows (byte apply).  The kernel
+timers prove the split kernels ran."""
+import numpy as np
+import pytest
+
+import libpoporon_amd as P
+
+pytestmark = pytest.mark.gpu
+
+# (symbol_size, poly, fcr, prim, num_roots), split path expected: RS(255,239),
+# t = 1, odd nr with fcr 5, nr 8 with fcr 3, prim 11 / 7 over other field
+# polynomials; and two sets outside the fast path's exponent bound
+# ((fcr + nr - 1) prim 254 >= 32768: RsCorrParams.vfast), which stay on the
+# general kernel with the same results
+PARAMS = [((8, 0x11D, 1, 1, 16), True), ((8, 0x11D, 0, 1, 2), True), ((8, 0x187, 5, 1, 31), True),
+          ((8, 0x11D, 3, 1, 8), True), ((8, 0x171, 1, 11, 10), True), ((8, 0x187, 1, 7, 16), True),
+          ((8, 0x187, 5, 7, 31), False), ((8, 0x171, 1, 11, 20), False)]
+
+
+@pytest.fixture(scope="module")
+def torch_cuda():
+    import torch
+    assert torch.cuda.is_available()
+    return torch
+
+
+def _channel(rng, data, par, nr, nmax):
+    """codewords with 0 .. nmax errors at random positions (data and parity)"""
+    n, k = data.shape
+    cw = np.concatenate([data, par], 1)
+    for c in range(n):
+        ne = min(c % (nmax + 1), k + nr)
+        pos = rng.permutation(k + nr)[:ne]
+        cw[c, pos] ^= rng.integers(1, 256, ne).astype(np.uint8)
+    return cw
+
+
+def _bm_launches(h):
+    return h.timing_read(P.KERNEL_BM)[1]
+
+
+@pytest.mark.parametrize("params,split", PARAMS)
+def test_nrsplit_vs_oracle(torch_cuda, params, split, monkeypatch):
+    """POPORON_AMD_DECODE_PATH=split sends every errors-only batch to the
+    split kernels: host batches and device batches (wire rows and strided
+    rows) at full length and shortened, bit-exact against the oracle."""
+    from oracle import Oracle
+    torch = torch_cuda
+    monkeypatch.setenv("POPORON_AMD_DECODE_PATH", "split")
+    m, poly, fcr, prim, nr = params
+    o, h = Oracle(*params), P.Poporon(*params)
+    assert h.supported
+    t = nr // 2
+    rng = np.random.default_rng(nr * 7919 + prim)
+    s = torch.cuda.current_stream().cuda_stream
+    for size in (255 - nr, (255 - nr) // 3, 1):
+        n = 3000
+        data = rng.integers(0, 256, (n, size), dtype=np.uint8)
+        par = o.encode_batch(data)
+        cw = _channel(rng, data, par, nr, t + 3)
+        ook, ocor, od, op = o.decode_batch(cw[:, :size], cw[:, size:])
+        assert (ook[(np.arange(n) % (t + 4)) <= t] == 1).all()  # within t: all corrected
+        # host batch
+        h.timing(True)
+        ok, cor, d, p = h.decode_batch(cw[:, :size], cw[:, size:])
+        assert (_bm_launches(h) > 0) == split, "split kernels ran" if not split else "split kernels did not run"
+        h.timing(False)
+        assert (ok == ook).all() and (cor == ocor).all(), size
+        assert (d == od).all() and (p == op).all(), size
+        # device batches: wire rows (size + nr bytes back to back) and strided rows
+        for extra, off in ((0, 0), (5, 3)):
+            w = size + nr + extra
+            buf = np.zeros(n * w + off + 64, np.uint8)
+            rows = buf[off:off + n * w].reshape(n, w)
+            rows[:, :size + nr] = cw
+            dev = torch.from_numpy(buf).cuda()
+            okd = torch.full((n,), 7, dtype=torch.uint8, device="cuda")
+            cord = torch.full((n,), 7, dtype=torch.uint8, device="cuda")
+            b = dev.data_ptr() + off
+            h.decode_batch_device(b, w, b + size, w, size, n, okd.data_ptr(), cord.data_ptr(), stream=s)
+            torch.cuda.synchronize()
+            got = dev.cpu().numpy()
+            grows = got[off:off + n * w].reshape(n, w)
+            assert (okd.cpu().numpy() == ook).all() and (cord.cpu().numpy() == ocor).all(), (size, extra)
+            assert (grows[:, :size] == od).all() and (grows[:, size:size + nr] == op).all(), (size, extra)
+            mask = np.ones(got.size, bool)  # nothing outside the codewords moved
+            mask[off:off + n * w].reshape(n, w)[:, :size + nr] = False
+            assert (got[mask] == buf[mask]).all(), (size, extra)
+
+
+@pytest.mark.parametrize("params", [(8, 0x11D, 1, 1, 16), (8, 0x187, 5, 1, 31)])
+def test_nrsplit_default_routing_large(torch_cuda, params):
+    """Without the override a batch of >= 16,384 codewords takes the split
+    kernels (a smaller one the general kernel): 40,000 wire rows with 0 .. t
+    errors all corrected, a sample equal to the oracle, the rest checked by
+    the round trip (bytes back to the encoded rows)."""
+    from oracle import Oracle
+    torch = torch_cuda
+    m, poly, fcr, prim, nr = params
+    o, h = Oracle(*params), P.Poporon(*params)
+    t = nr // 2
+    k = 255 - nr
+    n = 40000
+    rng = np.random.default_rng(nr)
+    data = rng.integers(0, 256, (n, k), dtype=np.uint8)
+    clean = np.concatenate([data, h.encode_batch(data)], 1)
+    assert (clean[::97, k:] == o.encode_batch(data[::97])).all()
+    cw = _channel(rng, data, clean[:, k:], nr, t)
+    s = torch.cuda.current_stream().cuda_stream
+    dev = torch.from_numpy(cw).cuda()
+    ok = torch.zeros(n, dtype=torch.uint8, device="cuda")
+    cor = torch.zeros(n, dtype=torch.uint8, device="cuda")
+    h.timing(True)
+    b = dev.data_ptr()
+    h.decode_batch_device(b, 255, b + k, 255, k, n, ok.data_ptr(), cor.data_ptr(), stream=s)
+    torch.cuda.synchronize()
+    assert _bm_launches(h) == 1
+    h.timing(False)
+    want_cor = np.array([((clean[c] != cw[c]).sum()) for c in range(n)], np.uint8)
+    assert bool((ok == 1).all())
+    assert (cor.cpu().numpy() == want_cor).all()
+    assert (dev.cpu().numpy() == clean).all()
+    ook, ocor, od, op = o.decode_batch(cw[::13, :k], cw[::13, k:])
+    assert (ook == 1).all() and (ocor == want_cor[::13]).all()
+    # below the split threshold: the general kernel, same results
+    h.timing(True)
+    small = torch.from_numpy(cw[:5000]).cuda()
+    ok2 = torch.zeros(5000, dtype=torch.uint8, device="cuda")
+    h.decode_batch_device(small.data_ptr(), 255, small.data_ptr() + k, 255, k, 5000, ok2.data_ptr(), stream=s)
+    torch.cuda.synchronize()
+    assert _bm_launches(h) == 0
+    h.timing(False)
+    assert bool((ok2 == 1).all()) and (small.cpu().numpy() == clean[:5000]).all()

@@ -1,12 +1,17 @@
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-for v in bp_px4 bp_px5 bp_px6; do
-  POPORON_AMD_LIB=$PWD/build/$v.so timeout -k 10 300 python -u -m pytest tests/test_gpu_split.py tests/test_gpu_parity.py -m gpu -x -q -k "era or erasure" --timeout 120 --timeout-method thread > gpurun_out/tests_$v.log 2>&1
-  rc=$?; echo "$v tests rc=$rc"; tail -2 gpurun_out/tests_$v.log
-  if [ $rc -ne 0 ]; then exit $rc; fi
-done
-for r in 1 2; do
-  timeout -k 10 600 python tools/exp_bench.py build/bp_base.so build/bp_px4.so build/bp_px5.so build/bp_px6.so > gpurun_out/bp_ab_$r.log 2>&1 || exit $?
-  cat gpurun_out/bp_ab_$r.log
-done
+timeout -k 10 300 python -u -m pytest tests/test_gpu_nrsplit.py -x -v --timeout 120 --timeout-method thread > gpurun_out/tests_nr.log 2>&1
+rc=$?; echo "nrsplit tests rc=$rc"; tail -12 gpurun_out/tests_nr.log
+if [ $rc -ne 0 ]; then exit $rc; fi
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/tests_all.log 2>&1
+rc=$?; echo "all tests rc=$rc"; tail -3 gpurun_out/tests_all.log
+if [ $rc -ne 0 ]; then exit $rc; fi
+timeout -k 10 600 python bench.py --no-c4 --no-host --no-latency --no-cpu-baseline > gpurun_out/bench_nr.log 2>&1; echo "bench rc=$?"
+python3 -c "
+import json
+l=[x for x in open('gpurun_out/bench_nr.log') if x.startswith('{')][-1]
+d=json.loads(l)
+print(d['value'], d['ms_per_step'], d['verified'])
+print(json.dumps(d.get('general_params')))
+"
