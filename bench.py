@@ -921,6 +921,19 @@ def general_params(be, n=1 << 20, reps=5, params=(8, 0x11D, 1, 1, 16), nerr=8):
         if r:
             td.append(time.perf_counter() - t0)
     nbad = be.n_bad((ok, cor), nerr) + be.n_diff(rows, clean)
+    # one more decode with the kernel events on: where the time goes
+    rows.copy_(bad)
+    be.sync()
+    h.timing(True)
+    h.decode_batch_device(b, N, b + k, N, k, n, ok.data_ptr(), cor.data_ptr(), stream=s)
+    be.sync()
+    kms = {}
+    for kid, name in P.KERNEL_NAMES.items():
+        ms, cnt = h.timing_read(kid)
+        if cnt:  # (the hand-off list of a code with < 32 roots runs on the general kernel)
+            kms[name.replace("rs_wave_k (list)", "rsg_decode_k (list)")] = round(ms / cnt, 4)
+    h.timing(False)
+    nbad += be.n_bad((ok, cor), nerr) + be.n_diff(rows, clean)
     idx = sample_index(n)
     o = Oracle(*params)
     smp_clean, smp_bad = be.host(clean, idx), be.host(bad, idx)
@@ -936,7 +949,7 @@ def general_params(be, n=1 << 20, reps=5, params=(8, 0x11D, 1, 1, 16), nerr=8):
                        "kernels with npar = nr (rsk_syndrome_reset_nr, rs_bm_k<true>, rs_chien_k, rs_forney_k, "
                        "rsk_apply_nr; hand-off list on rsg_decode_k)", "codewords": n, "errors_per_codeword": nerr,
             "encode_cw_per_s": round(n / e, 1), "decode_cw_per_s": round(n / d, 1),
-            "encode_ms": round(e * 1e3, 4), "decode_ms": round(d * 1e3, 4),
+            "encode_ms": round(e * 1e3, 4), "decode_ms": round(d * 1e3, 4), "decode_kernels_ms": kms,
             "hbm_frac_encode": round(n * N / e / 1e9 / HBM_PEAK_GBS, 4),
             "hbm_frac_decode": round(n * N / d / 1e9 / HBM_PEAK_GBS, 4),
             "timing": f"wall time per call, stream-synchronised, median of {reps}",

@@ -53,6 +53,9 @@ typedef __attribute__((address_space(1))) const uint32_t gu32;
 #define LFSR_STAGGER 0 /* (experiment) odd waves sleep LFSR_STAGGER x 8128 cycles first */
 #endif
 #define LFSR_REPL 16
+#ifndef LFSR_BLOCKS
+#define LFSR_BLOCKS 1 /* PATH_BLOCKS for sizes 16..256 other than the full RS(255,223) */
+#endif
 #ifndef LFSR_USTORE
 #define LFSR_USTORE 1
 #endif
@@ -398,6 +401,7 @@ __device__ __forceinline__ void store32_any(uint8_t *o, const uint32_t (&P)[8])
 #define PATH_GENERIC 0 /* any size, any alignment: dword loads per 16 bytes */
 #define PATH_SPLIT 1   /* size 223: data stream (rolling prefetch) + separate parity stream */
 #define PATH_CONTIG 2  /* size 223, parity right after the data: one 255-byte stream (rolling prefetch) */
+#define PATH_BLOCKS 3  /* 16 <= size <= 256 (shortened codes, fewer roots): 16-byte blocks, leading zeros */
 
 /* what the kernel does with the final register (encode: the parity bytes P, in order; syndrome / check: E') */
 template <int MODE>
@@ -499,6 +503,67 @@ __global__ __launch_bounds__(LFSR_WG) void rs_lfsr_k(const RsDevTables *__restri
             }
             lfsr_epilogue<MODE>(P, synt, cw, parity, pstride, out, npar);
         }
+    } else if (PATH == PATH_BLOCKS) {
+        /* The message as nb = ceil(size / 16) whole 16-byte blocks behind
+         * z = 16 nb - size leading zeros (a zero fed into a zero register
+         * leaves it zero, so the remainder is unchanged): block 0 is the
+         * message's first 16 bytes moved up by z bytes, block b > 0 the
+         * unaligned 16 bytes at msg - z + 16 b -- every load inside the
+         * message, all issued before the steps; the blocks' steps are
+         * unrolled (compile-time rotations) under wave-uniform guards. */
+        typedef unsigned u32x4u __attribute__((ext_vector_type(4), aligned(1)));
+        typedef __attribute__((address_space(1))) const u32x4u gu32x4u;
+        const uint32_t nb = (size + 15u) >> 4, z = 16u * nb - size;
+        const uint32_t zq = z >> 2, zs = 8u * (z & 3u);
+        uint32_t it = 0;
+        for (size_t cw = cw0; cw < count; cw += step, ++it) {
+            prio_by_progress(it);
+            const uint8_t *m = data + cw * dstride;
+            uint32_t V[16][4];
+            static_for<0, 16, 1>([&](auto bc) __attribute__((always_inline)) {
+                constexpr int b = decltype(bc)::value;
+                if ((uint32_t)b < nb) { /* uniform */
+                    const u32x4u v = *reinterpret_cast<gu32x4u *>((uintptr_t)(m + (b ? 16u * b - z : 0u)));
+                    V[b][0] = v.x, V[b][1] = v.y, V[b][2] = v.z, V[b][3] = v.w;
+                }
+            });
+            {   /* block 0 up by z bytes: dwords by zq (selects), then bytes by zs (64-bit funnels) */
+                uint32_t w[4];
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const uint32_t a = (zq & 1u) ? (k >= 1 ? V[0][k - 1] : 0u) : V[0][k];
+                    const uint32_t c = (zq & 1u) ? (k >= 3 ? V[0][k - 3] : 0u) : (k >= 2 ? V[0][k - 2] : 0u);
+                    w[k] = (zq & 2u) ? c : a;
+                }
+#pragma unroll
+                for (int k = 3; k >= 0; --k) {
+                    const uint64_t pair = ((uint64_t)w[k] << 32) | (k ? w[k - 1] : 0u);
+                    V[0][k] = (uint32_t)(pair >> (32u - zs));
+                }
+            }
+            uint32_t X[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+            uint32_t P[8];
+            static_for<0, 16, 1>([&](auto bc) __attribute__((always_inline)) {
+                constexpr int b = decltype(bc)::value;
+                if ((uint32_t)b < nb) {
+#pragma unroll
+                    for (int i = 0; i < 16; i += 2)
+                        il_pair(X, i, V[b][i >> 2] >> (8 * (i & 3)), V[b][(i + 1) >> 2] >> (8 * ((i + 1) & 3)), tab);
+                }
+            });
+            il_bytes(P, X, 0);
+            if (MODE != MODE_ENCODE) { /* E' = received parity + parity of the received data */
+                uint32_t Q[8];
+                if (npar < RS_NR)
+                    load_n_any(Q, parity + cw * pstride, npar);
+                else
+                    load32_any(Q, parity + cw * pstride);
+#pragma unroll
+                for (int q = 0; q < 8; ++q)
+                    P[q] ^= Q[q];
+            }
+            lfsr_epilogue<MODE>(P, synt, cw, parity, pstride, out, npar);
+        }
     } else if (PATH == PATH_CONTIG && MODE != MODE_ENCODE) {
         /* data || parity as one 255-byte stream */
         Stream<FULL_K + RS_NR> sc;
@@ -585,7 +650,10 @@ static hipError_t launch_lfsr(const RsDevTables *tab, const uint8_t *data, size_
         return hipSuccess;
     const dim3 grid(persistent_grid(count, LFSR_WG, num_cu)), block(LFSR_WG);
     uint8_t *par = const_cast<uint8_t *>(parity);
-    if (size != FULL_K || npar != RS_NR)
+    if ((size != FULL_K || npar != RS_NR) && size >= 16u && size <= 256u && LFSR_BLOCKS)
+        RS_LAUNCH((rs_lfsr_k<MODE, PATH_BLOCKS>), grid, block, 0, stream, tab, data, dstride, par, pstride,
+                           size, count, out, reset, npar);
+    else if (size != FULL_K || npar != RS_NR)
         RS_LAUNCH((rs_lfsr_k<MODE, PATH_GENERIC>), grid, block, 0, stream, tab, data, dstride, par, pstride,
                            size, count, out, reset, npar);
     else if (MODE != MODE_ENCODE && parity == data + FULL_K && pstride == dstride)

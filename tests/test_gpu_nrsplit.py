@@ -142,3 +142,46 @@ def test_nrsplit_default_routing_large(torch_cuda, params):
     assert _bm_launches(h) == 0
     h.timing(False)
     assert bool((ok2 == 1).all()) and (small.cpu().numpy() == clean[:5000]).all()
+
+
+@pytest.mark.parametrize("params", [(8, 0x11D, 1, 1, 32), (8, 0x11D, 1, 1, 16), (8, 0x187, 5, 1, 31), (8, 0x11D, 0, 1, 2)])
+def test_every_size_vs_oracle(torch_cuda, params, monkeypatch):
+    """Every message size 1 .. 255 - nr through the batch encode and the
+    split decode (POPORON_AMD_DECODE_PATH=split), rows at an odd offset and
+    stride: the LFSR kernel's block path (16 <= size <= 256 but not the full
+    RS(255,223): 16-byte blocks behind 16 nb - size leading zeros, every
+    z = 0..15) and its dword path (size < 16) against the oracle."""
+    from oracle import Oracle
+    torch = torch_cuda
+    monkeypatch.setenv("POPORON_AMD_DECODE_PATH", "split")
+    m, poly, fcr, prim, nr = params
+    o, h = Oracle(*params), P.Poporon(*params)
+    t = nr // 2
+    rng = np.random.default_rng(nr + 4242)
+    s = torch.cuda.current_stream().cuda_stream
+    n, off = 96, 3
+    for size in range(1, 256 - nr):
+        w = size + nr + 1
+        data = rng.integers(0, 256, (n, size), dtype=np.uint8)
+        want = o.encode_batch(data)
+        buf = np.zeros(n * w + off + 64, np.uint8)
+        rows = buf[off:off + n * w].reshape(n, w)
+        rows[:, :size] = data
+        dev = torch.from_numpy(buf).cuda()
+        b = dev.data_ptr() + off
+        h.encode_batch_device(b, w, b + size, w, size, n, s)
+        torch.cuda.synchronize()
+        got = dev.cpu().numpy()[off:off + n * w].reshape(n, w)
+        assert (got[:, size:size + nr] == want).all(), size
+        cw = _channel(rng, data, want, nr, t)
+        rows[:, :size + nr] = cw
+        dev = torch.from_numpy(buf).cuda()
+        ok = torch.zeros(n, dtype=torch.uint8, device="cuda")
+        cor = torch.zeros(n, dtype=torch.uint8, device="cuda")
+        b = dev.data_ptr() + off
+        h.decode_batch_device(b, w, b + size, w, size, n, ok.data_ptr(), cor.data_ptr(), stream=s)
+        torch.cuda.synchronize()
+        ook, ocor, od, op = o.decode_batch(cw[:, :size], cw[:, size:])
+        got = dev.cpu().numpy()[off:off + n * w].reshape(n, w)
+        assert (ok.cpu().numpy() == ook).all() and (cor.cpu().numpy() == ocor).all(), size
+        assert (got[:, :size] == od).all() and (got[:, size:size + nr] == op).all(), size
