@@ -1337,9 +1337,13 @@ static bool launch_decode(poporon_t *h, uint8_t *d_data, size_t ds, uint8_t *d_p
         return true;
     }
     if (h->nrsplit && !ext_syn && !pos8 && !pos32 && h->corr.vfast && !h->corr.force_verify &&
-        (h->decode_path == 1 || (h->decode_path == 0 && count >= SPLIT_MIN_COUNT))) {
+        (h->decode_path == 1 || h->decode_path == 0)) {
         /* a byte-symbol code of fewer than 32 roots, errors only: the split
-         * kernels with npar = num_roots, the list on the general kernel */
+         * kernels with npar = num_roots, the list on the general kernel --
+         * at every batch size, single calls included: the general kernel's
+         * one lane per codeword takes ~1 ms whatever the count, the six
+         * split launches ~0.1 ms from 1 to 65,536 codewords of RS(255,239)
+         * (profiles/r05_nr_batchlat.log) */
         RsCorrParams prm = h->corr;
         prm.size = (uint32_t)size;
         prm.pad = (int32_t)(h->rs->gf->field_size - h->rs->num_roots - size);

@@ -54,7 +54,10 @@ typedef __attribute__((address_space(1))) const uint32_t gu32;
 #endif
 #define LFSR_REPL 16
 #ifndef LFSR_BLOCKS
-#define LFSR_BLOCKS 1 /* PATH_BLOCKS for sizes 16..256 other than the full RS(255,223) */
+#define LFSR_BLOCKS 1 /* PATH_BLOCKS for sizes 16..256 other than the full RS(255,223) (0: the dword path) */
+#endif
+#ifndef LFSR_BLOCKS_ALL
+#define LFSR_BLOCKS_ALL 0 /* (experiment) PATH_BLOCKS for the full RS(255,223) too */
 #endif
 #ifndef LFSR_USTORE
 #define LFSR_USTORE 1
@@ -401,7 +404,7 @@ __device__ __forceinline__ void store32_any(uint8_t *o, const uint32_t (&P)[8])
 #define PATH_GENERIC 0 /* any size, any alignment: dword loads per 16 bytes */
 #define PATH_SPLIT 1   /* size 223: data stream (rolling prefetch) + separate parity stream */
 #define PATH_CONTIG 2  /* size 223, parity right after the data: one 255-byte stream (rolling prefetch) */
-#define PATH_BLOCKS 3  /* 16 <= size <= 256 (shortened codes, fewer roots): 16-byte blocks, leading zeros */
+#define PATH_BLOCKS 3  /* 16 <= size <= 256 (shortened codes, fewer roots): 16-byte blocks behind leading zeros, one kernel per block count */
 
 /* what the kernel does with the final register (encode: the parity bytes P, in order; syndrome / check: E') */
 template <int MODE>
@@ -411,10 +414,25 @@ __device__ __forceinline__ void lfsr_epilogue(const uint32_t (&P)[8], const uint
 {
     if (MODE == MODE_ENCODE && npar < RS_NR) {
         /* a generator of degree npar < 32 run as g(x) x^(32 - npar): its
-         * parity is the register's first npar bytes (rsk_encode_nr) */
+         * parity is the register's first npar bytes (rsk_encode_nr): whole
+         * dwords as unaligned dword stores (the first four as one 16-byte
+         * store), the last 0..3 bytes one by one */
+        typedef unsigned u32x4s __attribute__((ext_vector_type(4), aligned(1)));
+        typedef __attribute__((address_space(1))) u32x4s gu32x4s;
+        typedef __attribute__((address_space(1))) uint32_t gu32s __attribute__((aligned(1)));
         uint8_t *o = parity + cw * pstride;
-        for (uint32_t m = 0; m < npar; ++m)
-            o[m] = (uint8_t)(P[m >> 2] >> (8u * (m & 3u)));
+        const uint32_t nd = npar >> 2, nt = npar & 3u;
+        uint32_t tail = 0;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            if (k == 0 && nd >= 4u) /* uniform */
+                *(gu32x4s *)(uintptr_t)o = u32x4s{P[0], P[1], P[2], P[3]};
+            else if ((uint32_t)k < nd && !(k < 4 && nd >= 4u))
+                *(gu32s *)(uintptr_t)(o + 4 * k) = P[k];
+            tail = (uint32_t)k == nd ? P[k] : tail;
+        }
+        for (uint32_t b = 0; b < nt; ++b)
+            o[4u * nd + b] = (uint8_t)(tail >> (8u * b));
         return;
     }
     if (MODE == MODE_SYNDROME) {
@@ -456,7 +474,7 @@ __device__ __forceinline__ void lfsr_epilogue(const uint32_t (&P)[8], const uint
     }
 }
 
-template <int MODE, int PATH>
+template <int MODE, int PATH, int NB = 0>
 __global__ __launch_bounds__(LFSR_WG) void rs_lfsr_k(const RsDevTables *__restrict__ T,
                                                       const uint8_t *__restrict__ data, size_t dstride,
                                                       uint8_t *__restrict__ parity, size_t pstride, uint32_t size,
@@ -503,61 +521,87 @@ __global__ __launch_bounds__(LFSR_WG) void rs_lfsr_k(const RsDevTables *__restri
             }
             lfsr_epilogue<MODE>(P, synt, cw, parity, pstride, out, npar);
         }
-    } else if (PATH == PATH_BLOCKS) {
-        /* The message as nb = ceil(size / 16) whole 16-byte blocks behind
-         * z = 16 nb - size leading zeros (a zero fed into a zero register
-         * leaves it zero, so the remainder is unchanged): block 0 is the
-         * message's first 16 bytes moved up by z bytes, block b > 0 the
-         * unaligned 16 bytes at msg - z + 16 b -- every load inside the
-         * message, all issued before the steps; the blocks' steps are
-         * unrolled (compile-time rotations) under wave-uniform guards. */
-        typedef unsigned u32x4u __attribute__((ext_vector_type(4), aligned(1)));
-        typedef __attribute__((address_space(1))) const u32x4u gu32x4u;
-        const uint32_t nb = (size + 15u) >> 4, z = 16u * nb - size;
-        const uint32_t zq = z >> 2, zs = 8u * (z & 3u);
+    } else if constexpr (PATH == PATH_BLOCKS) {
+        /* The message as NB = ceil(size / 16) whole 16-byte blocks behind
+         * z = 16 NB - size leading zeros (a zero fed into a zero register
+         * leaves it zero: the remainder is unchanged), one kernel per NB (no
+         * guards, compile-time rotations).  The virtual stream starts at
+         * p = msg - z; chunk c is the aligned 16 bytes at align16(p) + 16 c,
+         * loaded only where it overlaps the message (and, for the syndromes
+         * of rows with the parity right behind the data, the parity), else
+         * msg's own chunk (in bounds, never fed); virtual dword j is the
+         * funnel of chunk dwords j + sdw, j + sdw + 1 by sb bytes (per lane:
+         * p's offset in its chunk); block 0's first z bytes (the previous
+         * row's, or a stand-in chunk's) are masked to zero.  The received
+         * parity is then virtual dwords 4 NB .. 4 NB + 7, or (elsewhere) loaded
+         * three blocks before the end. */
+        static_assert(NB >= 1 && NB <= 16, "PATH_BLOCKS: one kernel per block count");
+        constexpr int NC = MODE == MODE_ENCODE ? NB + 1 : NB + 3; /* chunks covering 15 + 16 NB (+ 32) bytes */
+        const uint32_t z = 16u * NB - size;
+        const bool pin = MODE != MODE_ENCODE && parity == data + size && pstride == dstride; /* uniform */
+        const uint32_t ext = size + (pin ? npar : 0u);
+        uint32_t zmask[4], pmask[8];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t lo = z > 4u * k ? min(z - 4u * k, 4u) : 0u; /* leading zero bytes of dword k */
+            zmask[k] = lo >= 4u ? 0u : ~0u << (8u * lo);
+        }
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const uint32_t hi = npar > 4u * k ? min(npar - 4u * k, 4u) : 0u; /* parity bytes of dword k */
+            pmask[k] = hi >= 4u ? ~0u : (1u << (8u * hi)) - 1u;
+        }
         uint32_t it = 0;
         for (size_t cw = cw0; cw < count; cw += step, ++it) {
             prio_by_progress(it);
-            const uint8_t *m = data + cw * dstride;
-            uint32_t V[16][4];
-            static_for<0, 16, 1>([&](auto bc) __attribute__((always_inline)) {
-                constexpr int b = decltype(bc)::value;
-                if ((uint32_t)b < nb) { /* uniform */
-                    const u32x4u v = *reinterpret_cast<gu32x4u *>((uintptr_t)(m + (b ? 16u * b - z : 0u)));
-                    V[b][0] = v.x, V[b][1] = v.y, V[b][2] = v.z, V[b][3] = v.w;
-                }
-            });
-            {   /* block 0 up by z bytes: dwords by zq (selects), then bytes by zs (64-bit funnels) */
-                uint32_t w[4];
-#pragma unroll
-                for (int k = 0; k < 4; ++k) {
-                    const uint32_t a = (zq & 1u) ? (k >= 1 ? V[0][k - 1] : 0u) : V[0][k];
-                    const uint32_t c = (zq & 1u) ? (k >= 3 ? V[0][k - 3] : 0u) : (k >= 2 ? V[0][k - 2] : 0u);
-                    w[k] = (zq & 2u) ? c : a;
-                }
-#pragma unroll
-                for (int k = 3; k >= 0; --k) {
-                    const uint64_t pair = ((uint64_t)w[k] << 32) | (k ? w[k - 1] : 0u);
-                    V[0][k] = (uint32_t)(pair >> (32u - zs));
-                }
-            }
+            const uintptr_t m = reinterpret_cast<uintptr_t>(data + cw * dstride);
+            const uintptr_t pv = m - z, c0 = pv & ~uintptr_t(15), mc = m & ~uintptr_t(15);
+            const uint32_t sdw = (uint32_t)(pv & 15u) >> 2, sb = (uint32_t)pv & 3u;
+            uint32_t D[4 * NC]; /* at(q) reads D[q .. q + 3]: q <= 4 NB (+ 8) */
+            auto chunk = [&](auto cc) __attribute__((always_inline)) {
+                constexpr int c = decltype(cc)::value;
+                const uintptr_t ca = c0 + 16u * c;
+                const bool in = ca < m + ext && ca + 16u > m;
+                const u32x4 v = *reinterpret_cast<gu32x4 *>(in ? ca : mc);
+                D[4 * c] = v.x, D[4 * c + 1] = v.y, D[4 * c + 2] = v.z, D[4 * c + 3] = v.w;
+            };
+            static_for<0, NB + 1, 1>(chunk); /* the message's chunks now, the parity's two later */
+            auto at = [&](int q) __attribute__((always_inline)) { /* chunk dword q + sdw */
+                const uint32_t t0 = (sdw & 1u) ? D[q + 1] : D[q];
+                const uint32_t t1 = (sdw & 1u) ? D[q + 3] : D[q + 2];
+                return (sdw & 2u) ? t1 : t0;
+            };
             uint32_t X[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-            uint32_t P[8];
-            static_for<0, 16, 1>([&](auto bc) __attribute__((always_inline)) {
+            uint32_t P[8], Q[8];
+            static_for<0, NB, 1>([&](auto bc) __attribute__((always_inline)) {
                 constexpr int b = decltype(bc)::value;
-                if ((uint32_t)b < nb) {
-#pragma unroll
-                    for (int i = 0; i < 16; i += 2)
-                        il_pair(X, i, V[b][i >> 2] >> (8 * (i & 3)), V[b][(i + 1) >> 2] >> (8 * ((i + 1) & 3)), tab);
+                if constexpr (MODE != MODE_ENCODE && b == (NB > 3 ? NB - 3 : 0)) {
+                    static_for<NB + 1, NC, 1>(chunk);
+                    if (!pin) { /* uniform */
+                        if (npar < RS_NR)
+                            load_n_any(Q, parity + cw * pstride, npar);
+                        else
+                            load32_any(Q, parity + cw * pstride);
+                    }
                 }
+                uint32_t W[4];
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    W[j] = __builtin_amdgcn_alignbyte(at(4 * b + j + 1), at(4 * b + j), sb);
+                    if (b == 0)
+                        W[j] &= zmask[j];
+                }
+#pragma unroll
+                for (int i = 0; i < 16; i += 2)
+                    il_pair(X, i, W[i >> 2] >> (8 * (i & 3)), W[(i + 1) >> 2] >> (8 * ((i + 1) & 3)), tab);
             });
             il_bytes(P, X, 0);
-            if (MODE != MODE_ENCODE) { /* E' = received parity + parity of the received data */
-                uint32_t Q[8];
-                if (npar < RS_NR)
-                    load_n_any(Q, parity + cw * pstride, npar);
-                else
-                    load32_any(Q, parity + cw * pstride);
+            if constexpr (MODE != MODE_ENCODE) { /* E' = received parity + parity of the received data */
+                if (pin) {
+#pragma unroll
+                    for (int k = 0; k < 8; ++k)
+                        Q[k] = __builtin_amdgcn_alignbyte(at(4 * NB + k + 1), at(4 * NB + k), sb) & pmask[k];
+                }
 #pragma unroll
                 for (int q = 0; q < 8; ++q)
                     P[q] ^= Q[q];
@@ -641,6 +685,22 @@ static int persistent_grid(size_t count, int wg, int num_cu) /* one round: 2 and
     return (int)(need < g ? (need ? need : 1) : g);
 }
 
+/* rs_lfsr_k<MODE, PATH_BLOCKS, NB> for NB = nb */
+template <int MODE, int NB>
+static void launch_blocks(uint32_t nb, dim3 grid, dim3 block, hipStream_t stream, const RsDevTables *tab,
+                          const uint8_t *data, size_t dstride, uint8_t *par, size_t pstride, uint32_t size,
+                          size_t count, uint8_t *out, uint32_t *reset, uint32_t npar)
+{
+    if constexpr (NB <= 16) {
+        if (nb == (uint32_t)NB)
+            RS_LAUNCH((rs_lfsr_k<MODE, PATH_BLOCKS, NB>), grid, block, 0, stream, tab, data, dstride, par, pstride,
+                      size, count, out, reset, npar);
+        else
+            launch_blocks<MODE, NB + 1>(nb, grid, block, stream, tab, data, dstride, par, pstride, size, count, out,
+                                        reset, npar);
+    }
+}
+
 template <int MODE>
 static hipError_t launch_lfsr(const RsDevTables *tab, const uint8_t *data, size_t dstride, const uint8_t *parity,
                               size_t pstride, uint32_t size, size_t count, uint8_t *out, int num_cu,
@@ -650,9 +710,9 @@ static hipError_t launch_lfsr(const RsDevTables *tab, const uint8_t *data, size_
         return hipSuccess;
     const dim3 grid(persistent_grid(count, LFSR_WG, num_cu)), block(LFSR_WG);
     uint8_t *par = const_cast<uint8_t *>(parity);
-    if ((size != FULL_K || npar != RS_NR) && size >= 16u && size <= 256u && LFSR_BLOCKS)
-        RS_LAUNCH((rs_lfsr_k<MODE, PATH_BLOCKS>), grid, block, 0, stream, tab, data, dstride, par, pstride,
-                           size, count, out, reset, npar);
+    if ((size != FULL_K || npar != RS_NR || LFSR_BLOCKS_ALL) && size >= 16u && size <= 256u && LFSR_BLOCKS)
+        launch_blocks<MODE, 1>((size + 15u) >> 4, grid, block, stream, tab, data, dstride, par, pstride, size, count,
+                               out, reset, npar);
     else if (size != FULL_K || npar != RS_NR)
         RS_LAUNCH((rs_lfsr_k<MODE, PATH_GENERIC>), grid, block, 0, stream, tab, data, dstride, par, pstride,
                            size, count, out, reset, npar);

@@ -100,11 +100,12 @@ def test_nrsplit_vs_oracle(torch_cuda, params, split, monkeypatch):
 
 
 @pytest.mark.parametrize("params", [(8, 0x11D, 1, 1, 16), (8, 0x187, 5, 1, 31)])
-def test_nrsplit_default_routing_large(torch_cuda, params):
-    """Without the override a batch of >= 16,384 codewords takes the split
-    kernels (a smaller one the general kernel): 40,000 wire rows with 0 .. t
-    errors all corrected, a sample equal to the oracle, the rest checked by
-    the round trip (bytes back to the encoded rows)."""
+def test_nrsplit_default_routing_large(torch_cuda, params, monkeypatch):
+    """Without the override every errors-only batch takes the split kernels:
+    40,000 wire rows with 0 .. t errors all corrected, a sample equal to the
+    oracle, the rest checked by the round trip (bytes back to the encoded
+    rows); POPORON_AMD_DECODE_PATH=single keeps a handle on the general
+    kernel, with the same results; single calls agree with the oracle."""
     from oracle import Oracle
     torch = torch_cuda
     m, poly, fcr, prim, nr = params
@@ -133,15 +134,23 @@ def test_nrsplit_default_routing_large(torch_cuda, params):
     assert (dev.cpu().numpy() == clean).all()
     ook, ocor, od, op = o.decode_batch(cw[::13, :k], cw[::13, k:])
     assert (ook == 1).all() and (ocor == want_cor[::13]).all()
-    # below the split threshold: the general kernel, same results
-    h.timing(True)
-    small = torch.from_numpy(cw[:5000]).cuda()
-    ok2 = torch.zeros(5000, dtype=torch.uint8, device="cuda")
-    h.decode_batch_device(small.data_ptr(), 255, small.data_ptr() + k, 255, k, 5000, ok2.data_ptr(), stream=s)
-    torch.cuda.synchronize()
-    assert _bm_launches(h) == 0
-    h.timing(False)
-    assert bool((ok2 == 1).all()) and (small.cpu().numpy() == clean[:5000]).all()
+    # a small batch: the split kernels too; forced onto the general kernel: same results
+    monkeypatch.setenv("POPORON_AMD_DECODE_PATH", "single")
+    hg = P.Poporon(*params)
+    monkeypatch.delenv("POPORON_AMD_DECODE_PATH")
+    for hh, launches in ((h, 1), (hg, 0)):
+        hh.timing(True)
+        small = torch.from_numpy(cw[:5000]).cuda()
+        ok2 = torch.zeros(5000, dtype=torch.uint8, device="cuda")
+        hh.decode_batch_device(small.data_ptr(), 255, small.data_ptr() + k, 255, k, 5000, ok2.data_ptr(), stream=s)
+        torch.cuda.synchronize()
+        assert _bm_launches(hh) == launches
+        hh.timing(False)
+        assert bool((ok2 == 1).all()) and (small.cpu().numpy() == clean[:5000]).all()
+    # single calls (poporon_decode): the split kernels on one codeword
+    for c in range(0, 64):
+        ok1, n1, d1, p1 = h.decode(cw[c, :k], cw[c, k:])
+        assert ok1 and n1 == want_cor[c] and (np.concatenate([d1, p1]) == clean[c]).all(), c
 
 
 @pytest.mark.parametrize("params", [(8, 0x11D, 1, 1, 32), (8, 0x11D, 1, 1, 16), (8, 0x187, 5, 1, 31), (8, 0x11D, 0, 1, 2)])
