@@ -558,14 +558,25 @@ __global__ __launch_bounds__(LFSR_WG) void rs_lfsr_k(const RsDevTables *__restri
             const uintptr_t pv = m - z, c0 = pv & ~uintptr_t(15), mc = m & ~uintptr_t(15);
             const uint32_t sdw = (uint32_t)(pv & 15u) >> 2, sb = (uint32_t)pv & 3u;
             uint32_t D[4 * NC]; /* at(q) reads D[q .. q + 3]: q <= 4 NB (+ 8) */
+            /* chunks cf .. cl overlap the row (cf = the chunk holding msg, 0 or 1) */
+            gu32x4 *cb = reinterpret_cast<gu32x4 *>(c0);
+            const uint32_t cf = (uint32_t)((mc - c0) >> 4), cl = (uint32_t)((((m + ext - 1u) & ~uintptr_t(15)) - c0) >> 4);
+            gu32x4 *ca[NC];
+            static_for<0, NC, 1>([&](auto cc) __attribute__((always_inline)) {
+                constexpr int c = decltype(cc)::value;
+                ca[c] = cb + (((uint32_t)c >= cf && (uint32_t)c <= cl) ? (uint32_t)c : cf);
+            });
+            __builtin_amdgcn_sched_barrier(0);
             auto chunk = [&](auto cc) __attribute__((always_inline)) {
                 constexpr int c = decltype(cc)::value;
-                const uintptr_t ca = c0 + 16u * c;
-                const bool in = ca < m + ext && ca + 16u > m;
-                const u32x4 v = *reinterpret_cast<gu32x4 *>(in ? ca : mc);
+                const u32x4 v = *ca[c];
                 D[4 * c] = v.x, D[4 * c + 1] = v.y, D[4 * c + 2] = v.z, D[4 * c + 3] = v.w;
             };
-            static_for<0, NB + 1, 1>(chunk); /* the message's chunks now, the parity's two later */
+            /* the message's chunks back to back (a row's chunks share its few
+             * cache lines: spread out, the lines leave the L1 between them),
+             * the parity's two later */
+            static_for<0, NB + 1, 1>(chunk);
+            __builtin_amdgcn_sched_barrier(0);
             auto at = [&](int q) __attribute__((always_inline)) { /* chunk dword q + sdw */
                 const uint32_t t0 = (sdw & 1u) ? D[q + 1] : D[q];
                 const uint32_t t1 = (sdw & 1u) ? D[q + 3] : D[q + 2];

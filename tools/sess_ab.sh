@@ -1,14 +1,15 @@
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-# the fused alternatives of the split decode: traffic and kernel times
-for path in single wave; do
-  for c in FETCH_SIZE WRITE_SIZE; do
-    lc=$(echo $c | cut -d_ -f1 | tr A-Z a-z)
-    POPORON_AMD_DECODE_PATH=$path timeout -k 10 200 rocprofv3 --pmc $c -d gpurun_out/fused_$path/roundtrip_$lc -o pmc --output-format csv -- python3 tools/kernel_driver.py --mode roundtrip --reps 3 > gpurun_out/fused_${path}_$lc.log 2>&1 || exit $?
-  done
-  python3 tools/pmc_traffic.py gpurun_out/fused_$path --json gpurun_out/fused_${path}_traffic.json > gpurun_out/fused_${path}_traffic.txt 2>&1
-  cat gpurun_out/fused_${path}_traffic.txt
-  POPORON_AMD_DECODE_PATH=$path timeout -k 10 200 rocprofv3 --kernel-trace --stats -d gpurun_out/fused_${path}_prof -o run --output-format csv -- python3 tools/kernel_driver.py --mode roundtrip --reps 3 > gpurun_out/fused_${path}_prof.log 2>&1 || exit $?
-  find gpurun_out/fused_${path}_prof -name "*kernel_stats.csv" -exec cat {} \; | cut -d, -f1-6 | head -12
-done
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/tests_all.log 2>&1
+rc=$?; echo "all tests rc=$rc"; tail -3 gpurun_out/tests_all.log
+if [ $rc -ne 0 ]; then exit $rc; fi
+timeout -k 10 600 python bench.py > gpurun_out/bench_full.log 2>&1; echo "bench rc=$?"
+python3 -c "
+import json
+l=[x for x in open('gpurun_out/bench_full.log') if x.startswith('{')][-1]
+d=json.loads(l)
+print(d['value'], d['ms_per_step'], d['verified'], d['roofline']['frac'])
+g=d['general_params']
+print(g['encode_cw_per_s'], g['decode_cw_per_s'], g['encode_ms'], g['decode_ms'], json.dumps(g['decode_kernels_ms']), g['verified'])
+"
