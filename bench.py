@@ -935,21 +935,47 @@ def general_params(be, n=1 << 20, reps=5, params=(8, 0x11D, 1, 1, 16), nerr=8):
     h.timing(False)
     nbad += be.n_bad((ok, cor), nerr) + be.n_diff(rows, clean)
     idx = sample_index(n)
+    got, gok, gcor = be.host(rows, idx), be.host(ok, idx), be.host(cor, idx)  # the error decode's sample
+    # erasure decode: nr sorted erasure slots in the data per codeword (the
+    # configs[3] shape for this code), u8 slots at stride nr
+    epos, emag = be.errors(0, n, nr, k, SEED + 42, sorted_positions=True)
+    ebad = clean.clone()
+    T.channel_xor(epos.data_ptr(), emag.data_ptr(), nr, ebad.data_ptr(), N, n, s)
+    ecnt = be.counts(n, nr)
+    tx = []
+    for r in range(reps + 1):
+        rows.copy_(ebad)
+        be.sync()
+        t0 = time.perf_counter()
+        h.decode_batch_device(b, N, b + k, N, k, n, ok.data_ptr(), cor.data_ptr(), d_positions=epos.data_ptr(),
+                              positions_stride=nr, d_counts=ecnt.data_ptr(), stream=s)
+        be.sync()
+        if r:
+            tx.append(time.perf_counter() - t0)
+    nbad += be.n_bad((ok, cor), nr) + be.n_diff(rows, clean)
     o = Oracle(*params)
     smp_clean, smp_bad = be.host(clean, idx), be.host(bad, idx)
     mism = int((o.encode_batch(smp_clean[:, :k]) != smp_clean[:, k:]).any(1).sum())
     ook, ocor, od, op = o.decode_batch(smp_bad[:, :k], smp_bad[:, k:])
-    got = be.host(rows, idx)
-    gok, gcor = be.host(ok, idx), be.host(cor, idx)
     mism += int(((ook != gok) | (ocor != gcor) | (od != got[:, :k]).any(1) | (op != got[:, k:]).any(1)).sum())
-    e, d = float(np.median(te)), float(np.median(td))
+    smp_ebad, smp_slots = be.host(ebad, idx), be.host(epos, idx)
+    xok, xcor, xd, xp = o.decode_batch(smp_ebad[:, :k], smp_ebad[:, k:], smp_slots.astype(np.uint32),
+                                       np.full(len(idx), nr, np.uint32))
+    got = be.host(rows, idx)
+    xgok, xgcor = be.host(ok, idx), be.host(cor, idx)
+    mism += int(((xok != xgok) | (xcor != xgcor) | (xd != got[:, :k]).any(1) | (xp != got[:, k:]).any(1)).sum())
+    e, d, x = float(np.median(te)), float(np.median(td)), float(np.median(tx))
     h.close()
     return {"code": f"RS(255,{k}): symbol_size {m}, poly {poly:#x}, fcr {fcr}, prim {prim}, {nr} roots",
             "kernels": "encode: rs_lfsr_k<ENCODE> with g(x) x^(32 - nr) (rsk_encode_nr); decode: the split "
                        "kernels with npar = nr (rsk_syndrome_reset_nr, rs_bm_k<true>, rs_chien_k, rs_forney_k, "
-                       "rsk_apply_nr; hand-off list on rsg_decode_k)", "codewords": n, "errors_per_codeword": nerr,
+                       "rsk_apply_nr; hand-off list on rsg_decode_k); erasure decode: the errata kernels with npar "
+                       "= nr (rsk_ebm_nr, rs_chien32_k, rsk_forney32_nr, rsk_apply_era_nr)", "codewords": n,
+            "errors_per_codeword": nerr,
             "encode_cw_per_s": round(n / e, 1), "decode_cw_per_s": round(n / d, 1),
             "encode_ms": round(e * 1e3, 4), "decode_ms": round(d * 1e3, 4), "decode_kernels_ms": kms,
+            "erasure_decode_cw_per_s": round(n / x, 1), "erasure_decode_ms": round(x * 1e3, 4),
+            "erasures_per_codeword": nr,
             "hbm_frac_encode": round(n * N / e / 1e9 / HBM_PEAK_GBS, 4),
             "hbm_frac_decode": round(n * N / d / 1e9 / HBM_PEAK_GBS, 4),
             "timing": f"wall time per call, stream-synchronised, median of {reps}",

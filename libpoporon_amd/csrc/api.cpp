@@ -1310,8 +1310,8 @@ static bool launch_split(poporon_t *h, const RsCorrParams &prm, const RsSplitWs 
             RsGenParams gp = h->gen;
             gp.size = (uint32_t)size;
             gp.pad = prm.pad;
-            HIP_OK(rsg_decode_list(g.gtab, &gp, d_data, ds, d_par, ps, count, ws.list, ws.nlist, ok, corrected,
-                                   g.num_cu, s));
+            HIP_OK(rsg_decode_list(g.gtab, &gp, d_data, ds, d_par, ps, count, ws.list, ws.nlist, nullptr, 0, nullptr,
+                                   ok, corrected, g.num_cu, s));
         } else {
             HIP_OK(rsk_wave(g.tab, &prm, d_data, ds, d_par, ps, count, ws.list, ws.nlist, ws.syn, nullptr, 0, nullptr,
                             nullptr, 0, nullptr, ok, corrected, g.num_cu, s));
@@ -1358,6 +1358,63 @@ static bool launch_decode(poporon_t *h, uint8_t *d_data, size_t ds, uint8_t *d_p
         if (!launch_split(h, prm, ws, d_data, ds, d_par, ps, size, count, ok, corrected, s, h->rs->num_roots))
             return false;
         return !shared || rem_release(h->gpu, s);
+    }
+    if (h->nrsplit && pos8 && !ext_syn && h->corr.vfast && !h->corr.force_verify &&
+        (h->decode_path == 1 || h->decode_path == 0) && pos_stride >= h->rs->num_roots && pos_stride % 4u == 0u &&
+        (reinterpret_cast<uintptr_t>(pos8) & 3u) == 0u) {
+        /* ... and its erasure batches (u8 slots in 4-byte aligned rows): the
+         * errata kernels with npar = num_roots, the list on the general
+         * kernel in erasure mode, the 32-entry record apply */
+        const uint32_t nr = h->rs->num_roots;
+        RsCorrParams prm = h->corr;
+        prm.size = (uint32_t)size;
+        prm.pad = (int32_t)(h->rs->gf->field_size - nr - size);
+        GpuCtx &g = h->gpu;
+        const bool shared = !rem;
+        if (shared) {
+            if (!ensure_rem(h, count) || !rem_acquire(g, s))
+                return false;
+            rem = g.rem;
+            rem_cap = g.rem_cap;
+        }
+        const RsSplitWs ws = rs_ws_carve(rem, rem_cap ? rem_cap : count);
+        {
+            KernelTimer t(g, POPORON_AMD_KERNEL_REMAINDER, s);
+            HIP_OK(rsk_syndrome_reset_nr(g.tab, d_data, ds, d_par, ps, (uint32_t)size, count, ws.syn, ws.nlist, nr,
+                                         g.num_cu, s));
+            t.done();
+        }
+        {
+            KernelTimer t(g, POPORON_AMD_KERNEL_BM, s);
+            HIP_OK(rsk_ebm_nr(g.tab, &prm, &ws, pos8, pos_stride, cnt, count, ok, corrected, nr, g.num_cu, s));
+            t.done();
+        }
+        {
+            KernelTimer t(g, POPORON_AMD_KERNEL_CHIEN, s);
+            HIP_OK(rsk_chien32(g.tab, &prm, &ws, count, ok, corrected, 0u, g.num_cu, s));
+            t.done();
+        }
+        {
+            KernelTimer t(g, POPORON_AMD_KERNEL_FORNEY, s);
+            HIP_OK(rsk_forney32_nr(g.tab, &prm, &ws, pos8, pos_stride, count, ok, corrected, nr, g.num_cu, s));
+            t.done();
+        }
+        {
+            /* the hand-off (meta RS_ST_LIST: the record apply passes them by) */
+            KernelTimer t(g, POPORON_AMD_KERNEL_LIST, s);
+            RsGenParams gp = h->gen;
+            gp.size = (uint32_t)size;
+            gp.pad = prm.pad;
+            HIP_OK(rsg_decode_list(g.gtab, &gp, d_data, ds, d_par, ps, count, ws.list, ws.nlist, pos8, pos_stride, cnt,
+                                   ok, corrected, g.num_cu, s));
+            t.done();
+        }
+        {
+            KernelTimer t(g, POPORON_AMD_KERNEL_APPLY, s);
+            HIP_OK(rsk_apply_era_nr(&prm, ws.meta, ws.ext, d_data, ds, d_par, ps, count, nr, s));
+            t.done();
+        }
+        return !shared || rem_release(g, s);
     }
     if (!h->fast) {
         RsGenParams prm = h->gen;

@@ -290,6 +290,18 @@ hipError_t rsk_bm_nr(const RsDevTables *tab, const RsSplitWs *ws, size_t count, 
                      uint8_t *corrected, int num_cu, hipStream_t stream);
 hipError_t rsk_apply_nr(const RsCorrParams *prm, const RsSplitWs *ws, uint8_t *data, size_t dstride, uint8_t *parity,
                         size_t pstride, size_t count, uint32_t npar, hipStream_t stream);
+/* and its errata decode (erasure batches, u8 slots, pos_stride >= npar, 4-byte
+ * aligned rows of slots): rsk_ebm_nr, rsk_chien32, rsk_forney32_nr, the list
+ * on the general kernel (rsg_decode_list in erasure mode), rsk_apply_era_nr */
+hipError_t rsk_ebm_nr(const RsDevTables *tab, const RsCorrParams *prm, const RsSplitWs *ws, const uint8_t *pos8,
+                      size_t pos_stride, const uint8_t *cnt, size_t count, uint8_t *ok, uint8_t *corrected,
+                      uint32_t npar, int num_cu, hipStream_t stream);
+hipError_t rsk_forney32_nr(const RsDevTables *tab, const RsCorrParams *prm, const RsSplitWs *ws, const uint8_t *pos8,
+                           size_t pos_stride, size_t count, uint8_t *ok, uint8_t *corrected, uint32_t npar,
+                           int num_cu, hipStream_t stream);
+hipError_t rsk_apply_era_nr(const RsCorrParams *prm, const uint8_t *meta, const uint8_t *rec, uint8_t *data,
+                            size_t dstride, uint8_t *parity, size_t pstride, size_t count, uint32_t npar,
+                            hipStream_t stream);
 
 /*
  * Split erasure-mode decode, after rsk_syndrome into ws.syn:

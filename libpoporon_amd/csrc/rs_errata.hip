@@ -71,7 +71,7 @@ __global__ __launch_bounds__(XWG, 4) void rs_ebm_k(const RsDevTables *__restrict
                                                   uint8_t *__restrict__ ext, uint8_t *__restrict__ meta,
                                                   uint32_t *__restrict__ list, uint32_t *__restrict__ nlist,
                                                   uint8_t *__restrict__ ok, uint8_t *__restrict__ corrected,
-                                                  uint32_t only_pend)
+                                                  uint32_t only_pend, uint32_t npar)
 {
     if (only_pend && nlist[1] == 0u) /* rs_era_bp_k decoded every codeword */
         return;
@@ -82,7 +82,7 @@ __global__ __launch_bounds__(XWG, 4) void rs_ebm_k(const RsDevTables *__restrict
     const uint32_t pofs = gf.pofs;
     const uint32_t AZ = gf.az();
     constexpr uint32_t DQZ = SZ; /* "no update": dq + B's logs read zeros */
-    const uint32_t lim = P.size + RS_NR, pad = (uint32_t)P.pad;
+    const uint32_t lim = P.size + npar, pad = (uint32_t)P.pad;
 
     uint32_t it = 0;
     for (size_t base = (size_t)blockIdx.x * XWG; base < count; base += (size_t)gridDim.x * XWG, ++it) {
@@ -100,14 +100,15 @@ __global__ __launch_bounds__(XWG, 4) void rs_ebm_k(const RsDevTables *__restrict
             const uint32_t *pw = reinterpret_cast<const uint32_t *>(pos8 + cw * pos_stride);
 #pragma unroll
             for (int k = 0; k < RS_NR / 4; ++k)
-                pk[k] = pw[k];
+                if (4u * k < npar) /* uniform: the row holds npar slots (a code of npar < 32 roots) */
+                    pk[k] = pw[k];
         }
         const bool any = (sa.x | sa.y | sa.z | sa.w | sb.x | sb.y | sb.z | sb.w) != 0u;
         bool inside = true; /* every erasure slot inside the codeword: L_l = slot + pad <= 254 */
 #pragma unroll
         for (int n = 0; n < RS_NR; ++n)
             inside = inside && ((uint32_t)n >= ne || ((pk[n >> 2] >> (8 * (n & 3))) & 0xffu) < lim);
-        const bool elig = valid && any && ne <= RS_NR && inside;
+        const bool elig = valid && any && ne <= npar && inside;
         if (valid && !any) { /* zero syndromes: success whatever the list says (src/decode.c:468) */
             ok[cw] = 1;
             if (corrected)
@@ -179,7 +180,7 @@ __global__ __launch_bounds__(XWG, 4) void rs_ebm_k(const RsDevTables *__restrict
             WL[k] = SZ | (SZ << 16);
         auto step = [&](auto sc, uint32_t r) __attribute__((always_inline)) {
             constexpr int s = decltype(sc)::value;
-            const bool act = elig && r > ne;
+            const bool act = elig && r > ne && r <= npar;
             const uint32_t ub = wave_max_full(act ? dl : 0u);
             /* logs of the old coefficients: the discrepancy's terms and B's copy;
              * AZ above the wave's degree bound (those coefficients are zero) */
@@ -246,10 +247,11 @@ __global__ __launch_bounds__(XWG, 4) void rs_ebm_k(const RsDevTables *__restrict
             }
         };
         uint32_t snext = sp[0];
+        const uint32_t nq = (npar + 3u) >> 2; /* iterations r <= npar (a step past npar changes nothing: act) */
 #pragma unroll 1
-        for (uint32_t q = 0; q < RS_NR / 4; ++q) {
+        for (uint32_t q = 0; q < nq; ++q) {
             const uint32_t sd = snext;
-            if (q + 1u < RS_NR / 4) /* uniform */
+            if (q + 1u < nq) /* uniform */
                 snext = sp[q + 1u];
 #pragma unroll
             for (int k = 17; k >= 2; --k)
@@ -520,7 +522,8 @@ __global__ __launch_bounds__(XWG, 4) void rs_forney32_k(const RsDevTables *__res
                                                        size_t count, uint8_t *__restrict__ ext,
                                                        const uint8_t *__restrict__ roots,
                                                        uint8_t *__restrict__ meta, uint8_t *__restrict__ ok,
-                                                       uint8_t *__restrict__ corrected, const uint32_t *__restrict__ npend)
+                                                       uint8_t *__restrict__ corrected, const uint32_t *__restrict__ npend,
+                                                       uint32_t npar)
 {
     if (npend && *npend == 0u) /* rs_era_bp_k decoded every codeword */
         return;
@@ -628,8 +631,9 @@ __global__ __launch_bounds__(XWG, 4) void rs_forney32_k(const RsDevTables *__res
             const uint32_t *pw = reinterpret_cast<const uint32_t *>(pos8 + cw * pos_stride);
             uint32_t X[RS_NR / 4];
 #pragma unroll
-            for (int k = 0; k < RS_NR / 4; ++k) /* reversed: byte j = slot 31 - j */
-                X[k] = __builtin_amdgcn_perm(0u, pw[RS_NR / 4 - 1 - k], 0x00010203u);
+            for (int k = 0; k < RS_NR / 4; ++k) /* reversed: byte j = slot 31 - j (the row's npar slots only) */
+                X[k] = __builtin_amdgcn_perm(0u, 4u * (RS_NR / 4 - 1 - k) < npar ? pw[RS_NR / 4 - 1 - k] : 0u,
+                                             0x00010203u);
             const uint32_t sh = RS_NR - deg; /* bytes: X <- X >> 8 sh, 0xFF shifted in */
 #pragma unroll
             for (int bit = 1; bit < 16; bit <<= 1) {
@@ -671,7 +675,22 @@ extern "C" hipError_t rsk_ebm(const RsDevTables *tab, const RsCorrParams *prm, c
     if (count == 0)
         return hipSuccess;
     RS_LAUNCH(rs_ebm_k, dim3(errata_grid(count, num_cu)), dim3(XWG), 0, stream, tab, *prm, ws->syn, pos8,
-                       pos_stride, cnt, count, ws->ext, ws->meta, ws->list, ws->nlist, ok, corrected, only_pend);
+                       pos_stride, cnt, count, ws->ext, ws->meta, ws->list, ws->nlist, ok, corrected, only_pend,
+                       (uint32_t)RS_NR);
+    return hipGetLastError();
+}
+
+/* a byte-symbol code of npar < 32 roots (syndromes from rsk_syndrome_reset_nr,
+ * rows of npar slots, pos_stride >= npar): npar iterations, at most npar
+ * erasures; Chien (rsk_chien32) as for 32 */
+extern "C" hipError_t rsk_ebm_nr(const RsDevTables *tab, const RsCorrParams *prm, const RsSplitWs *ws,
+                                 const uint8_t *pos8, size_t pos_stride, const uint8_t *cnt, size_t count, uint8_t *ok,
+                                 uint8_t *corrected, uint32_t npar, int num_cu, hipStream_t stream)
+{
+    if (count == 0)
+        return hipSuccess;
+    RS_LAUNCH(rs_ebm_k, dim3(errata_grid(count, num_cu)), dim3(XWG), 0, stream, tab, *prm, ws->syn, pos8,
+              pos_stride, cnt, count, ws->ext, ws->meta, ws->list, ws->nlist, ok, corrected, 0u, npar);
     return hipGetLastError();
 }
 
@@ -692,6 +711,18 @@ extern "C" hipError_t rsk_forney32(const RsDevTables *tab, const RsCorrParams *p
     if (count == 0)
         return hipSuccess;
     RS_LAUNCH(rs_forney32_k, dim3(errata_grid(count, num_cu)), dim3(XWG), 0, stream, tab, *prm, pos8,
-                       pos_stride, count, ws->ext, ws->roots, ws->meta, ok, corrected, only_pend ? ws->nlist + 1 : nullptr);
+                       pos_stride, count, ws->ext, ws->roots, ws->meta, ok, corrected, only_pend ? ws->nlist + 1 : nullptr,
+                       (uint32_t)RS_NR);
+    return hipGetLastError();
+}
+
+extern "C" hipError_t rsk_forney32_nr(const RsDevTables *tab, const RsCorrParams *prm, const RsSplitWs *ws,
+                                      const uint8_t *pos8, size_t pos_stride, size_t count, uint8_t *ok,
+                                      uint8_t *corrected, uint32_t npar, int num_cu, hipStream_t stream)
+{
+    if (count == 0)
+        return hipSuccess;
+    RS_LAUNCH(rs_forney32_k, dim3(errata_grid(count, num_cu)), dim3(XWG), 0, stream, tab, *prm, pos8, pos_stride,
+              count, ws->ext, ws->roots, ws->meta, ok, corrected, (const uint32_t *)nullptr, npar);
     return hipGetLastError();
 }

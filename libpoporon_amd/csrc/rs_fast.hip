@@ -1002,6 +1002,13 @@ extern "C" hipError_t rsk_apply_nr(const RsCorrParams *prm, const RsSplitWs *ws,
     return apply_launch<16>(prm, ws->meta, ws->roots, data, dstride, parity, pstride, count, stream, npar);
 }
 
+extern "C" hipError_t rsk_apply_era_nr(const RsCorrParams *prm, const uint8_t *meta, const uint8_t *rec, uint8_t *data,
+                                       size_t dstride, uint8_t *parity, size_t pstride, size_t count, uint32_t npar,
+                                       hipStream_t stream)
+{
+    return apply_launch<32>(prm, meta, rec, data, dstride, parity, pstride, count, stream, npar);
+}
+
 extern "C" hipError_t rsk_apply_era(const RsCorrParams *prm, const uint8_t *meta, const uint8_t *rec, uint8_t *data,
                                     size_t dstride, uint8_t *parity, size_t pstride, size_t count, hipStream_t stream)
 {

@@ -40,11 +40,13 @@ hipError_t rsg_decode(const RsGenTables *tab, const RsGenParams *prm, uint8_t *d
                       size_t pstride, size_t count, const uint16_t *ext, size_t ext_stride, const uint8_t *pos8,
                       const uint32_t *pos32, size_t pos_stride, const uint8_t *cnt, uint8_t *ok, uint8_t *corrected,
                       int num_cu, hipStream_t stream);
-/* errors-only decode of the codewords list[0 .. *list_n) (the split decode's
- * hand-off for codes of fewer than 32 roots; length read on the device) */
+/* decode of the codewords list[0 .. *list_n) (the split decode's hand-off for
+ * codes of fewer than 32 roots; length read on the device): errors only
+ * (pos8 NULL) or with u8 erasure slots */
 hipError_t rsg_decode_list(const RsGenTables *tab, const RsGenParams *prm, uint8_t *data, size_t dstride,
                            uint8_t *parity, size_t pstride, size_t count, const uint32_t *list, const uint32_t *list_n,
-                           uint8_t *ok, uint8_t *corrected, int num_cu, hipStream_t stream);
+                           const uint8_t *pos8, size_t pos_stride, const uint8_t *cnt, uint8_t *ok,
+                           uint8_t *corrected, int num_cu, hipStream_t stream);
 
 /* dirty[c] = any syndrome nonzero (may be NULL); syn (may be NULL): the
  * nroots log-form syndromes of codeword c at syn[c*syn_stride ..] */

@@ -194,3 +194,70 @@ def test_every_size_vs_oracle(torch_cuda, params, monkeypatch):
         got = dev.cpu().numpy()[off:off + n * w].reshape(n, w)
         assert (ok.cpu().numpy() == ook).all() and (cor.cpu().numpy() == ocor).all(), size
         assert (got[:, :size] == od).all() and (got[:, size:size + nr] == op).all(), size
+
+
+@pytest.mark.parametrize("params", [(8, 0x11D, 1, 1, 16), (8, 0x187, 5, 1, 31), (8, 0x11D, 3, 1, 8),
+                                    (8, 0x171, 1, 11, 10), (8, 0x11D, 0, 1, 2)])
+@pytest.mark.parametrize("split", [True, False])
+def test_nrsplit_erasures_vs_oracle(torch_cuda, params, split, monkeypatch):
+    """Erasure batches of a code with fewer than 32 roots (u8 slots) on the
+    errata kernels with npar = nr (rsk_ebm_nr, rsk_chien32, rsk_forney32_nr,
+    the list on rsg_decode_k in erasure mode, rsk_apply_era_nr), or, with
+    POPORON_AMD_DECODE_PATH=single, on the general kernel: bytes, ok and
+    corrected_num equal the oracle's over erasure counts 0 .. nr + 2 (past
+    nr: refused when dirty, quirk Q5), errors besides (within and past the
+    capability), unsorted and repeated slots (Q1), slots read past the count
+    (Q2), slots past the codeword, shortened sizes, rows of slots at a stride
+    of roundup(nr, 4) (the errata path) and nr + 1 (the general kernel)."""
+    from oracle import Oracle
+    torch = torch_cuda
+    monkeypatch.setenv("POPORON_AMD_DECODE_PATH", "split" if split else "single")
+    m, poly, fcr, prim, nr = params
+    o, h = Oracle(*params), P.Poporon(*params)
+    rng = np.random.default_rng(nr * 31 + fcr)
+    s = torch.cuda.current_stream().cuda_stream
+    for size in (255 - nr, (255 - nr) // 2):
+        n = 2000
+        data = rng.integers(0, 256, (n, size), dtype=np.uint8)
+        cw = np.concatenate([data, o.encode_batch(data)], 1)
+        slots = np.zeros((n, nr), np.uint8)
+        cnts = np.zeros(n, np.uint8)
+        for c in range(n):
+            e = c % (nr + 3)
+            pos = rng.permutation(size + nr)[:min(e, size + nr)]
+            if c % 3:
+                pos = np.sort(pos)
+            if c % 7 == 0 and len(pos) > 1:
+                pos[-1] = pos[0]  # a repeated slot
+            if c % 11 == 0 and len(pos):
+                pos[-1] = min(255, size + nr + int(rng.integers(0, 8)))  # past the codeword
+            k = min(len(pos), nr)
+            slots[c, :k] = pos[:k]
+            slots[c, k:] = rng.integers(0, size, nr - k)  # stale entries past the count
+            cnts[c] = e
+            inside = pos[pos < size + nr]
+            cw[c, inside] ^= rng.integers(1, 256, len(inside)).astype(np.uint8)
+            room = max(0, (nr - min(e, nr)) // 2 + (1 if c % 5 == 0 else 0))  # one past the capability at times
+            free = np.setdiff1d(np.arange(size + nr), pos)
+            pe = rng.permutation(free)[:room]
+            cw[c, pe] ^= rng.integers(1, 256, len(pe)).astype(np.uint8)
+        ook, ocor, od, op = o.decode_batch(cw[:, :size], cw[:, size:], slots.astype(np.uint32), cnts.astype(np.uint32))
+        for ps in ((nr + 3) // 4 * 4, nr + 1):
+            sl = np.zeros((n, ps), np.uint8)
+            sl[:, :nr] = slots
+            dev = torch.from_numpy(np.ascontiguousarray(cw)).cuda()
+            dsl = torch.from_numpy(sl).cuda()
+            dcn = torch.from_numpy(cnts).cuda()
+            ok = torch.full((n,), 7, dtype=torch.uint8, device="cuda")
+            cor = torch.full((n,), 7, dtype=torch.uint8, device="cuda")
+            b = dev.data_ptr()
+            h.timing(True)
+            h.decode_batch_device(b, size + nr, b + size, size + nr, size, n, ok.data_ptr(), cor.data_ptr(),
+                                  d_positions=dsl.data_ptr(), positions_stride=ps, d_counts=dcn.data_ptr(), stream=s)
+            torch.cuda.synchronize()
+            errata = _bm_launches(h) > 0
+            h.timing(False)
+            assert errata == (split and ps % 4 == 0), (size, ps)
+            got = dev.cpu().numpy()
+            assert (ok.cpu().numpy() == ook).all() and (cor.cpu().numpy() == ocor).all(), (size, ps)
+            assert (got[:, :size] == od).all() and (got[:, size:] == op).all(), (size, ps)
