@@ -2376,6 +2376,7 @@ static bool rs_decode_one(poporon_t *h, uint8_t *data, size_t size, uint8_t *par
             uint8_t *hs = g.hstage;
             const uint16_t *ext = nullptr;
             const uint32_t *pos32 = nullptr;
+            const uint8_t *pos8 = nullptr;
             const uint8_t *cnt = nullptr;
             bool refuse = false;
             size_t in_bytes = off_cor + 1;
@@ -2397,13 +2398,29 @@ static bool rs_decode_one(poporon_t *h, uint8_t *data, size_t size, uint8_t *par
                 in_bytes = off_x + nr * 4 + 1;
                 pos32 = (const uint32_t *)(g.stage + off_x);
                 cnt = g.stage + off_x + nr * 4;
+                /* a fewer-roots code whose nr slots (the count's and the stale
+                 * ones the reference reads, Q2) all fit a byte below 255: u8
+                 * slots, so the errata kernels take it (launch_decode) */
+                const uint32_t *pv = reinterpret_cast<const uint32_t *>(hs + off_x);
+                bool small = h->nrsplit;
+                for (size_t i = 0; i < nr && small; i++)
+                    small = pv[i] < 255u;
+                if (small) {
+                    uint8_t sl[RS_NR];
+                    for (size_t i = 0; i < nr; i++)
+                        sl[i] = (uint8_t)pv[i];
+                    memset(hs + off_x, 0, nr * 4);
+                    memcpy(hs + off_x, sl, nr); /* a row of nr u8 slots, 4-byte aligned, stride nr * 4 */
+                    pos32 = nullptr;
+                    pos8 = g.stage + off_x;
+                }
             }
             if (refuse) {
                 fail("external syndrome > field size: undefined in the reference, refused");
             } else {
                 HIP_OK(hipMemcpyAsync(g.stage, hs, in_bytes, hipMemcpyHostToDevice, g.stream));
-                if (!launch_decode(h, g.stage, size, g.stage + off_p, nr, size, 1, ext, nr, nullptr, pos32, nr, cnt,
-                                   g.stage + off_ok, g.stage + off_cor, g.stream))
+                if (!launch_decode(h, g.stage, size, g.stage + off_p, nr, size, 1, ext, nr, pos8, pos32,
+                                   pos8 ? nr * 4 : nr, cnt, g.stage + off_ok, g.stage + off_cor, g.stream))
                     return false;
                 HIP_OK(hipMemcpyAsync(hs, g.stage, off_cor + 1, hipMemcpyDeviceToHost, g.stream));
                 HIP_OK(hipStreamSynchronize(g.stream));

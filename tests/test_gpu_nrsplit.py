@@ -261,3 +261,41 @@ def test_nrsplit_erasures_vs_oracle(torch_cuda, params, split, monkeypatch):
             got = dev.cpu().numpy()
             assert (ok.cpu().numpy() == ook).all() and (cor.cpu().numpy() == ocor).all(), (size, ps)
             assert (got[:, :size] == od).all() and (got[:, size:] == op).all(), (size, ps)
+
+
+@pytest.mark.parametrize("params", [(8, 0x11D, 1, 1, 16), (8, 0x187, 5, 1, 31)])
+def test_nrsplit_single_call_erasures_vs_oracle(torch_cuda, params):
+    """poporon_decode with an erasure object on a code with fewer than 32
+    roots: slots below 255 go to the errata kernels as u8 slots, a slot of
+    255 or more keeps the general kernel's u32 path; either way the bytes,
+    the result and corrected_num equal the oracle's (stale slots past the
+    count included, quirk Q2; counts past nr, Q5)."""
+    from oracle import Oracle
+    m, poly, fcr, prim, nr = params
+    o = Oracle(*params)
+    er = P.Erasure(nr, nr)
+    h = P.Poporon(*params, erasure=er)
+    rng = np.random.default_rng(nr + 99)
+    k = 255 - nr
+    for c in range(120):
+        data = rng.integers(0, 256, (1, k), dtype=np.uint8)
+        cw = np.concatenate([data, o.encode_batch(data)], 1)[0]
+        e = c % (nr + 2)
+        pos = np.sort(rng.permutation(k)[:min(e, k)])
+        slots = np.zeros(nr, np.uint32)
+        slots[:min(e, nr)] = pos[:nr]
+        slots[min(e, nr):] = rng.integers(0, k, nr - min(e, nr))
+        if c % 9 == 0:
+            slots[-1] = 300  # a slot past a byte: the u32 path
+        cw[pos] ^= rng.integers(1, 256, len(pos)).astype(np.uint8)
+        ne = max(0, (nr - e) // 2)
+        free = np.setdiff1d(np.arange(255), pos)
+        pe = rng.permutation(free)[:ne]
+        cw[pe] ^= rng.integers(1, 256, ne).astype(np.uint8)
+        er.set(slots)
+        er.set(slots[:e] if e <= nr else np.concatenate([slots, rng.integers(0, k, e - nr).astype(np.uint32)]))
+        ok, n, d, p = h.decode(cw[:k], cw[k:])
+        cnt = np.array([e], np.uint32)
+        ook, ocor, od, op = o.decode_batch(cw[None, :k], cw[None, k:], slots[None, :].astype(np.uint32), cnt)
+        assert ok == bool(ook[0]) and n == ocor[0], c
+        assert (d == od[0]).all() and (p == op[0]).all(), c
