@@ -42,7 +42,7 @@ def main():
         nonlocal cur
         if cur:
             names = [k for k, _ in cur]
-            if any(k == "rs_bm_k" for k in names):
+            if any(re.match(r"rs_bm_k\b", k) for k in names):  # rs_bm_k<false> (32 roots) / <true> (fewer)
                 mode = "decode16"
             elif any(k == "rs_ebm_k" and d > 20e3 for k, d in cur):
                 mode = "errata16e8"
