@@ -1568,6 +1568,9 @@ EXPORT bool poporon_check_batch_device(poporon_t *h, const uint8_t *d_data, size
     if (h->fast) {
         HIP_OK(rsk_check(h->gpu.tab, d_data, data_stride, d_parity, parity_stride, (uint32_t)size, count, d_dirty,
                          h->gpu.num_cu, s));
+    } else if (h->nrsplit) {
+        HIP_OK(rsk_check_nr(h->gpu.tab, d_data, data_stride, d_parity, parity_stride, (uint32_t)size, count, d_dirty,
+                            h->rs->num_roots, h->gpu.num_cu, s));
     } else {
         RsGenParams prm = h->gen;
         prm.size = (uint32_t)size;
@@ -1595,6 +1598,19 @@ EXPORT bool poporon_syndrome_batch_device(poporon_t *h, const uint8_t *d_data, s
         return false;
     DeviceGuard dg(h->gpu.device);
     hipStream_t s = (hipStream_t)stream;
+    if (h->nrsplit) { /* fewer roots: the LFSR kernel's npar syndromes, then their logs */
+        if (!ensure_rem(h, count) || !rem_acquire(h->gpu, s))
+            return false;
+        {
+            KernelTimer t(h->gpu, POPORON_AMD_KERNEL_REMAINDER, s);
+            HIP_OK(rsk_syndrome_reset_nr(h->gpu.tab, d_data, data_stride, d_parity, parity_stride, (uint32_t)size,
+                                         count, h->gpu.rem, nullptr, h->rs->num_roots, h->gpu.num_cu, s));
+            t.done();
+        }
+        HIP_OK(rsk_syn_log_nr(h->gpu.tab, h->gpu.rem, count, d_syndromes, syndrome_stride, d_nonzero,
+                              h->rs->num_roots, s));
+        return rem_release(h->gpu, s);
+    }
     if (!h->fast) {
         RsGenParams prm = h->gen;
         prm.size = (uint32_t)size;

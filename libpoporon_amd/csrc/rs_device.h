@@ -234,6 +234,13 @@ hipError_t rsk_syn_log(const RsDevTables *tab, const uint8_t *syn, size_t count,
 /* flag[c] = remainder of codeword c is nonzero */
 hipError_t rsk_check(const RsDevTables *tab, const uint8_t *data, size_t dstride, const uint8_t *parity, size_t pstride,
                      uint32_t size, size_t count, uint8_t *flag, int num_cu, hipStream_t stream);
+/* the same two for a byte-symbol code of npar < 32 roots (tables of
+ * build_tables_nr): log-form syndromes S_0..S_(npar-1), the remainder flag */
+hipError_t rsk_syn_log_nr(const RsDevTables *tab, const uint8_t *syn, size_t count, uint16_t *out, size_t stride,
+                          uint8_t *flag, uint32_t npar, hipStream_t stream);
+hipError_t rsk_check_nr(const RsDevTables *tab, const uint8_t *data, size_t dstride, const uint8_t *parity,
+                        size_t pstride, uint32_t size, size_t count, uint8_t *flag, uint32_t npar, int num_cu,
+                        hipStream_t stream);
 
 /*
  * Correction.  syn: 32 syndromes per codeword, poly form (from rsk_syndrome);

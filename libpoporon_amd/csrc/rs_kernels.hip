@@ -786,7 +786,7 @@ extern "C" hipError_t rsk_syndrome_reset_nr(const RsDevTables *tab, const uint8_
  * uint16 log S_i (255 = zero) and the "any nonzero" flag (src/decode.c:409-414) */
 __global__ __launch_bounds__(256) void rs_synlog_k(const RsDevTables *__restrict__ T, const uint8_t *__restrict__ syn,
                                                    size_t count, uint16_t *__restrict__ out, size_t stride,
-                                                   uint8_t *__restrict__ flag)
+                                                   uint8_t *__restrict__ flag, uint32_t nout)
 {
     __shared__ uint8_t lg[256];
     lg[threadIdx.x] = T->log[threadIdx.x];
@@ -798,7 +798,7 @@ __global__ __launch_bounds__(256) void rs_synlog_k(const RsDevTables *__restrict
     for (uint32_t i = 0; i < RS_NR; ++i) {
         const uint32_t v = syn[cw * RS_NR + i];
         any |= v;
-        if (out)
+        if (out && i < nout) /* nout = num_roots (zeros behind the syndromes of a code with fewer roots) */
             out[cw * stride + i] = lg[v];
     }
     if (flag)
@@ -811,7 +811,18 @@ extern "C" hipError_t rsk_syn_log(const RsDevTables *tab, const uint8_t *syn, si
     if (count == 0)
         return hipSuccess;
     const size_t blocks = (count + 255) / 256;
-    RS_LAUNCH(rs_synlog_k, dim3((uint32_t)blocks), dim3(256), 0, stream, tab, syn, count, out, stride, flag);
+    RS_LAUNCH(rs_synlog_k, dim3((uint32_t)blocks), dim3(256), 0, stream, tab, syn, count, out, stride, flag,
+              (uint32_t)RS_NR);
+    return hipGetLastError();
+}
+
+extern "C" hipError_t rsk_syn_log_nr(const RsDevTables *tab, const uint8_t *syn, size_t count, uint16_t *out,
+                                     size_t stride, uint8_t *flag, uint32_t npar, hipStream_t stream)
+{
+    if (count == 0)
+        return hipSuccess;
+    const size_t blocks = (count + 255) / 256;
+    RS_LAUNCH(rs_synlog_k, dim3((uint32_t)blocks), dim3(256), 0, stream, tab, syn, count, out, stride, flag, npar);
     return hipGetLastError();
 }
 
@@ -820,4 +831,14 @@ extern "C" hipError_t rsk_check(const RsDevTables *tab, const uint8_t *data, siz
                                 hipStream_t stream)
 {
     return launch_lfsr<MODE_CHECK>(tab, data, dstride, parity, pstride, size, count, flag, num_cu, stream);
+}
+
+/* a code of npar < 32 roots: E' = the received parity + the data's, npar
+ * bytes (the flag equals "any syndrome nonzero": distinct roots) */
+extern "C" hipError_t rsk_check_nr(const RsDevTables *tab, const uint8_t *data, size_t dstride, const uint8_t *parity,
+                                   size_t pstride, uint32_t size, size_t count, uint8_t *flag, uint32_t npar,
+                                   int num_cu, hipStream_t stream)
+{
+    return launch_lfsr<MODE_CHECK>(tab, data, dstride, parity, pstride, size, count, flag, num_cu, stream, nullptr,
+                                   npar);
 }

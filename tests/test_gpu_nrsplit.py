@@ -299,3 +299,37 @@ def test_nrsplit_single_call_erasures_vs_oracle(torch_cuda, params):
         ook, ocor, od, op = o.decode_batch(cw[None, :k], cw[None, k:], slots[None, :].astype(np.uint32), cnt)
         assert ok == bool(ook[0]) and n == ocor[0], c
         assert (d == od[0]).all() and (p == op[0]).all(), c
+
+
+@pytest.mark.parametrize("params", [(8, 0x11D, 1, 1, 16), (8, 0x187, 5, 1, 31), (8, 0x11D, 0, 1, 2)])
+def test_nrsplit_check_and_syndromes_vs_oracle(torch_cuda, params):
+    """poporon_check_batch_device and poporon_syndrome_batch_device of a code
+    with fewer than 32 roots on the LFSR kernel (rsk_check_nr,
+    rsk_syndrome_reset_nr + rsk_syn_log_nr): the dirty flags and the npar
+    log-form syndromes (rows of exactly nr entries, the next row right
+    behind) equal the oracle's, full-length and shortened, clean and dirty."""
+    from oracle import Oracle
+    torch = torch_cuda
+    m, poly, fcr, prim, nr = params
+    o, h = Oracle(*params), P.Poporon(*params)
+    rng = np.random.default_rng(nr + 7)
+    s = torch.cuda.current_stream().cuda_stream
+    for size in (255 - nr, 40):
+        n = 3000
+        data = rng.integers(0, 256, (n, size), dtype=np.uint8)
+        cw = np.concatenate([data, o.encode_batch(data)], 1)
+        for c in range(n):
+            ne = c % 4
+            cw[c, rng.permutation(size + nr)[:ne]] ^= rng.integers(1, 256, ne).astype(np.uint8)
+        dev = torch.from_numpy(cw).cuda()
+        b, w = dev.data_ptr(), size + nr
+        dirty = torch.full((n,), 7, dtype=torch.uint8, device="cuda")
+        h.check_batch_device(b, w, b + size, w, size, n, dirty.data_ptr(), s)
+        syn = torch.zeros((n, nr), dtype=torch.int16, device="cuda")
+        nz = torch.full((n,), 7, dtype=torch.uint8, device="cuda")
+        h.syndrome_batch_device(b, w, b + size, w, size, n, syn.data_ptr(), nr, nz.data_ptr(), s)
+        torch.cuda.synchronize()
+        got_syn = syn.cpu().numpy().astype(np.uint16)
+        for c in range(n):
+            f, want = o.syndrome(cw[c, :size], cw[c, size:])
+            assert bool(dirty[c]) == f and bool(nz[c]) == f and (got_syn[c] == want).all(), (size, c)
