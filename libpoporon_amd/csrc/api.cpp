@@ -494,6 +494,7 @@ static void build_decode_tables(poporon_t *h, uint32_t nr)
     p.prim = rs->primitive_element;
     p.iprim = h->primitive_inverse;
     p.vfast = ((uint64_t)(p.fcr + nr - 1) * p.prim * 254u) < 32768u;
+    p.nr = nr;
 
     /* E' -> syndrome nibble tables (rs_device.h) */
     auto gmul = [&](uint32_t x, uint32_t logc) -> uint8_t {
@@ -650,6 +651,21 @@ static void build_lfsr_rows(poporon_t *h)
                     ((uint32_t)row[k + 24] << 24);
         memcpy(&t.lfsr[fb * 2], il, 16);
         memcpy(&t.lfsr[fb * 2 + 1], il + 4, 16);
+    }
+    /* encq: parity (log form, 255 = zero, stride 32) of the message 1 followed
+     * by d zeros, d < 255 - nr: the same LFSR steps (rs_enc1_k) */
+    memset(t.encq, 255, sizeof(t.encq));
+    uint8_t q[RS_NR];
+    for (uint32_t m = 0; m < nr; m++) /* one step with feedback 1 */
+        q[m] = (uint8_t)gf->log2exp[gf_mod(gf, g[nr - 1 - m])];
+    for (uint32_t d = 0; d < 255u - nr; d++) {
+        for (uint32_t m = 0; m < nr; m++)
+            t.encq[d * RS_NR + m] = (uint8_t)gf->exp2log[q[m]];
+        const uint32_t fb = q[0]; /* next step, input byte 0 */
+        for (uint32_t m = 0; m < nr; m++) {
+            const uint8_t sh = m + 1 < nr ? q[m + 1] : 0;
+            q[m] = sh ^ (fb == 0 ? 0 : (uint8_t)gf->log2exp[gf_mod(gf, (uint16_t)(gf->exp2log[fb] + g[nr - 1 - m]))]);
+        }
     }
 }
 
@@ -1240,7 +1256,9 @@ static bool launch_encode(poporon_t *h, const uint8_t *d_data, size_t ds, uint8_
         HIP_OK(rsk_encode1(h->gpu.tab, d_data, d_par, (uint32_t)size, nullptr, 0, s));
     } else if (h->fast) {
         HIP_OK(rsk_encode(h->gpu.tab, d_data, ds, d_par, ps, (uint32_t)size, count, h->gpu.num_cu, s));
-    } else if (h->lfsr_nr && count > 1) {
+    } else if (h->lfsr_nr && count == 1 && size <= 255u - h->rs->num_roots) { /* one codeword: the whole workgroup */
+        HIP_OK(rsk_encode1_nr(h->gpu.tab, d_data, d_par, (uint32_t)size, h->rs->num_roots, nullptr, 0u, s));
+    } else if (h->lfsr_nr) {
         HIP_OK(rsk_encode_nr(h->gpu.tab, d_data, ds, d_par, ps, (uint32_t)size, count, h->rs->num_roots,
                              h->gpu.num_cu, s));
     } else {
@@ -1333,6 +1351,18 @@ static bool launch_decode(poporon_t *h, uint8_t *d_data, size_t ds, uint8_t *d_p
             return fail("BCH has no erasure or external-syndrome decode");
         KernelTimer t(h->gpu, POPORON_AMD_KERNEL_CORRECT, s);
         HIP_OK(bchk_decode(&h->bch, d_data, ds, d_par, ps, count, ok, corrected, h->gpu.num_cu, s));
+        t.done();
+        return true;
+    }
+    if (h->nrsplit && count == 1 && h->decode_path == 0) {
+        /* one codeword of a fewer-roots code: the whole reference decode on
+         * one workgroup (rs_dec1_k with P.nr = num_roots; every mode) */
+        RsCorrParams prm = h->corr;
+        prm.size = (uint32_t)size;
+        prm.pad = (int32_t)(h->rs->gf->field_size - h->rs->num_roots - size);
+        KernelTimer t(h->gpu, POPORON_AMD_KERNEL_SINGLE, s);
+        HIP_OK(rsk_decode1(h->gpu.tab, &prm, ext_syn ? 2u : (pos8 || pos32) ? 1u : 0u, d_data, d_par, pos8, pos32,
+                           cnt, 1u, ext_syn, ok, corrected, nullptr, 0, s));
         t.done();
         return true;
     }
@@ -2255,7 +2285,8 @@ EXPORT bool poporon_encode(poporon_t *h, uint8_t *data, size_t size, uint8_t *pa
     /* one RS codeword: rs_enc1_k reads the message from and writes the parity
      * to coherent host memory and signals its completion word there (one
      * launch, no copies, no stream synchronisation) */
-    if (h->fec_type == PPLN_FEC_RS && h->fast && size >= 1 && size <= 223 && ensure_zc(g)) {
+    /* (codes with fewer roots, h->nrsplit, the same way: their encq rows, P.nr) */
+    if (h->fec_type == PPLN_FEC_RS && (h->fast || h->nrsplit) && size >= 1 && size <= kmax(h) && ensure_zc(g)) {
         memcpy(g.zc + ZC_DATA, data, size);
         if (serve_enabled() && !g.timing) {
             if (!srv_call(h, RS_SRV_ENCODE, (uint32_t)size, 0u))
@@ -2263,8 +2294,8 @@ EXPORT bool poporon_encode(poporon_t *h, uint8_t *data, size_t size, uint8_t *pa
         } else {
             const uint32_t seq = ++g.zc_seq;
             KernelTimer t(g, POPORON_AMD_KERNEL_ENCODE, g.stream);
-            HIP_OK(rsk_encode1(g.tab, g.zc_dev + ZC_DATA, g.zc_dev + ZC_PAR, (uint32_t)size,
-                               reinterpret_cast<uint32_t *>(g.zc_dev + ZC_FLAG), seq, g.stream));
+            HIP_OK(rsk_encode1_nr(g.tab, g.zc_dev + ZC_DATA, g.zc_dev + ZC_PAR, (uint32_t)size, (uint32_t)nr,
+                                  reinterpret_cast<uint32_t *>(g.zc_dev + ZC_FLAG), seq, g.stream));
             t.done();
             if (!zc_wait(g, seq))
                 return false;
@@ -2334,7 +2365,7 @@ static bool rs_decode_one(poporon_t *h, uint8_t *data, size_t size, uint8_t *par
         DeviceGuard dg(h->gpu.device);
         GpuCtx &g = h->gpu;
         const size_t nr = h->rs->num_roots;
-        if (h->fast && ensure_zc(g)) {
+        if ((h->fast || h->nrsplit) && ensure_zc(g)) {
             /* rs_dec1_k: the whole decode of one codeword in one launch, reading
              * the codeword, the erasure slots or the external syndromes from
              * coherent host memory and writing back the corrected bytes, ok and
@@ -2362,7 +2393,7 @@ static bool rs_decode_one(poporon_t *h, uint8_t *data, size_t size, uint8_t *par
             prm.size = (uint32_t)size;
             prm.pad = (int32_t)(h->rs->gf->field_size - h->rs->num_roots - size);
             uint8_t *zd = g.zc_dev;
-            if (serve_enabled() && !g.timing && size == prm.size && prm.pad == (int32_t)(RS_NN - RS_NR - size)) {
+            if (serve_enabled() && !g.timing && size == prm.size && prm.pad == (int32_t)(RS_NN - nr - size)) {
                 if (!srv_call(h, RS_SRV_DECODE, (uint32_t)size, mode))
                     return false;
             } else {

@@ -82,7 +82,7 @@ struct RsDevTables {
     /* encq[d * 32 + m]: log (255 = zero) of parity byte m of the one-byte
      * message 1 followed by d zero bytes (d < 223): the LFSR is GF-linear, so
      * one codeword's parity is sum_j data_j encq[size - 1 - j] (rs_enc1_k) */
-    uint8_t encq[223 * 32];
+    uint8_t encq[255 * 32]; /* d < 223 (fast codes); d < 255 - nr for a code of nr < 32 roots, bytes m >= nr 255 */
 };
 #define RS_Z0 200u /* zero sentinel row of gfa (rs_fast.hip) */
 
@@ -94,6 +94,7 @@ struct RsCorrParams {
     int32_t pad;     /* 255 - 32 - size */
     uint32_t vfast;  /* (fcr+31)*prim*254 < 32768: verification exponents need no int16 emulation */
     uint32_t force_verify; /* run the re-syndrome check even where it provably passes (tests) */
+    uint32_t nr;     /* num_roots: 32, or fewer (rs_dec1_k of a fewer-roots code) */
 };
 
 /*
@@ -179,6 +180,9 @@ hipError_t rsk_syndrome_reset(const RsDevTables *tab, const uint8_t *data, size_
  *                one byte each */
 hipError_t rsk_encode1(const RsDevTables *tab, const uint8_t *data, uint8_t *parity, uint32_t size, uint32_t *flag,
                        uint32_t seq, hipStream_t stream);
+/* the same for a code of npar < 32 roots (encq of build_lfsr_rows), size <= 255 - npar */
+hipError_t rsk_encode1_nr(const RsDevTables *tab, const uint8_t *data, uint8_t *parity, uint32_t size, uint32_t npar,
+                          uint32_t *flag, uint32_t seq, hipStream_t stream);
 hipError_t rsk_decode1(const RsDevTables *tab, const RsCorrParams *prm, uint32_t mode, uint8_t *data,
                        uint8_t *parity, const uint8_t *pos8, const uint32_t *pos32, const void *cnt,
                        uint32_t cnt_bytes, const uint16_t *ext, uint8_t *ok, uint8_t *corrected, uint32_t *flag,

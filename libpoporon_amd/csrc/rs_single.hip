@@ -128,7 +128,7 @@ __device__ __forceinline__ void fill_tabs(Tabs &s, const RsDevTables *__restrict
 /* the encode of one message by the whole workgroup; the tables in s are
  * filled (or being filled: the first barrier below orders them) */
 __device__ __forceinline__ void enc1_body(Tabs &s, uint32_t (*wred)[8], const RsDevTables *__restrict__ T,
-                                          const uint8_t *data, uint8_t *parity, uint32_t size)
+                                          const uint8_t *data, uint8_t *parity, uint32_t size, uint32_t npar = RS_NR)
 {
     const uint32_t t = threadIdx.x, lane = t & 63u, wave = t >> 6;
     uint32_t w = 0;
@@ -164,20 +164,21 @@ __device__ __forceinline__ void enc1_body(Tabs &s, uint32_t (*wred)[8], const Rs
         wred[wave][lane] = v;
     }
     __syncthreads();
-    if (t < RS_NR) {
+    if (t < npar) { /* npar < 32: a code with fewer roots (its encq rows are zero past npar) */
         const uint32_t d = wred[0][t >> 2] ^ wred[1][t >> 2] ^ wred[2][t >> 2] ^ wred[3][t >> 2];
         parity[t] = (uint8_t)(d >> (8u * (t & 3u)));
     }
 }
 
 __global__ __launch_bounds__(S1_WG) void rs_enc1_k(const RsDevTables *__restrict__ T, const uint8_t *data,
-                                                   uint8_t *parity, uint32_t size, uint32_t *flag, uint32_t seq)
+                                                   uint8_t *parity, uint32_t size, uint32_t *flag, uint32_t seq,
+                                                   uint32_t npar)
 {
     __shared__ Tabs s;
     __shared__ uint32_t wred[4][8];
     const uint32_t t = threadIdx.x;
     fill_tabs(s, T, t);
-    enc1_body(s, wred, T, data, parity, size);
+    enc1_body(s, wred, T, data, parity, size, npar);
     if (flag) {
         /* every wave's parity stores acknowledged, then lane 0's system-scope
          * release and the flag (rs_serve_k) */
@@ -224,7 +225,8 @@ __device__ void dec1_body(Dec1Smem &s, const RsCorrParams &P, uint32_t mode, uin
                           const uint16_t *ext, uint8_t *okp, uint8_t *corp)
 {
     const uint32_t t = threadIdx.x, lane = t & 63u, wave = t >> 6;
-    const uint32_t size = P.size, L = size + RS_NR;
+    const uint32_t nr = P.nr; /* 32, or fewer (a code with fewer roots: syndromes, BM, check over nr) */
+    const uint32_t size = P.size, L = size + nr;
     const int32_t pad = P.pad;
     uint32_t ok = 0, fixed = 0;
     /* STAMP 0 */
@@ -237,9 +239,9 @@ __device__ void dec1_body(Dec1Smem &s, const RsCorrParams &P, uint32_t mode, uin
     uint32_t ne = 0, xs = 0;
     if (mode == 1u) {
         ne = cnt_bytes == 4u ? *(const uint32_t *)cnt : *(const uint8_t *)cnt;
-        if (t < RS_NR)
+        if (t < nr)
             s.pos[t] = pos32 ? pos32[t] : pos8[t];
-    } else if (mode == 2u && t < RS_NR) {
+    } else if (mode == 2u && t < nr) {
         xs = ext[t];
     }
     s.cw[t] = (uint8_t)w;
@@ -247,7 +249,7 @@ __device__ void dec1_body(Dec1Smem &s, const RsCorrParams &P, uint32_t mode, uin
         s.flags = 0;
         s.low = 0;
     }
-    if (t >= RS_NR && t < 64u)
+    if (t >= nr && t < 64u)
         s.slog[t] = ZL;
     __syncthreads();
     /* STAMP 1 */
@@ -255,7 +257,7 @@ __device__ void dec1_body(Dec1Smem &s, const RsCorrParams &P, uint32_t mode, uin
     /* ---- syndromes, log form (src/decode.c:375-415; external: :446-454) ---- */
     bool refuse = false;
     if (mode == 2u) {
-        if (t < RS_NR) {
+        if (t < nr) {
             refuse = xs > 255u; /* out-of-table in the reference: refused */
             s.slog[t] = xs >= 255u ? ZL : xs;
             s.spoly[t] = xs >= 255u ? 0u : s.g.ex[xs];
@@ -280,7 +282,7 @@ __device__ void dec1_body(Dec1Smem &s, const RsCorrParams &P, uint32_t mode, uin
         }
         s.part[t] = acc;
         __syncthreads();
-        if (t < RS_NR) {
+        if (t < nr) {
             uint32_t v = 0;
 #pragma unroll
             for (int k = 0; k < 8; ++k)
@@ -299,7 +301,7 @@ __device__ void dec1_body(Dec1Smem &s, const RsCorrParams &P, uint32_t mode, uin
         /* a clean codeword succeeds whatever its erasure count (src/decode.c:468);
          * a dirty one with more erasures than roots overflows the reference's
          * locator (quirk Q5): refused, as the batch kernels do */
-        if (!any || (mode == 1u && ne > RS_NR)) {
+        if (!any || (mode == 1u && ne > nr)) {
             ok = any ? 0u : 1u;
             goto finish;
         }
@@ -308,7 +310,7 @@ __device__ void dec1_body(Dec1Smem &s, const RsCorrParams &P, uint32_t mode, uin
     /* ---- erasure locator and Berlekamp-Massey on wave 0: lane i holds
      * Lambda_i (poly and log) and B_i (log), i <= 32 ---- */
     if (wave == 0) {
-        const bool co = lane <= RS_NR; /* a coefficient lane */
+        const bool co = lane <= nr; /* a coefficient lane */
         uint32_t lam = lane == 0 ? 1u : 0u;
         /* Lambda = prod (1 + X_l x), X_l = alpha^(prim (254 - (pos_l + pad))) with the
          * reference's uint32 arithmetic and uint16 gf_mod (src/decode.c:34-47) */
@@ -330,14 +332,14 @@ __device__ void dec1_body(Dec1Smem &s, const RsCorrParams &P, uint32_t mode, uin
         uint32_t term = s.g.ex[llam + s.slog[lane <= ne ? ne - lane : 63u]]; /* Lambda_i S_(r-1-i), r = ne + 1 */
         /* S_(r-i) for the terms of the next iteration, read one iteration
          * ahead (slog[63] = ZL past them) */
-        uint32_t s1 = s.slog[lane <= ne + 1u && ne + 1u < RS_NR ? ne + 1u - lane : 63u];
-        for (uint32_t r = ne + 1u; r <= RS_NR; ++r) {
+        uint32_t s1 = s.slog[lane <= ne + 1u && ne + 1u < nr ? ne + 1u - lane : 63u];
+        for (uint32_t r = ne + 1u; r <= nr; ++r) {
             const uint32_t disc = wave_xor_v(term); /* in every lane */
             const uint32_t bs = wave_up_old(B, ZL);  /* B_(i-1); lane 0: zero (Lambda_0 stays 1) */
             const uint32_t ld = s.g.lg[disc];
             const uint32_t dq = red(ld + bs);         /* log of disc B_(i-1); >= 255: zero */
             const uint32_t t1 = s.g.ex[llam + s1], t2 = s.g.ex[dq + s1], up = s.g.ex[dq];
-            s1 = s.slog[lane <= r + 1u && r + 1u < RS_NR ? r + 1u - lane : 63u];
+            s1 = s.slog[lane <= r + 1u && r + 1u < nr ? r + 1u - lane : 63u];
             term = t1 ^ t2;
             const uint32_t ds = __builtin_amdgcn_readfirstlane(disc);
             const bool len = ds != 0u && 2u * Lr <= r + ne - 1u; /* uniform */
@@ -350,8 +352,8 @@ __device__ void dec1_body(Dec1Smem &s, const RsCorrParams &P, uint32_t mode, uin
         /* degree, src/decode.c:98-110 (lane 0 holds Lambda_0 = 1) */
         const uint64_t nz = __ballot(co && lam != 0u);
         const uint32_t deg = 63u - (uint32_t)__builtin_clzll(nz);
-        if (co)
-            s.llam[lane] = llam;
+        if (lane <= RS_NR) /* ZL past nr: Chien, Omega and Forney read up to Lambda_32 */
+            s.llam[lane] = co ? llam : ZL;
         if (lane == 0) {
             s.deg = deg;
             s.nfix = 0;
@@ -487,7 +489,7 @@ __device__ void dec1_body(Dec1Smem &s, const RsCorrParams &P, uint32_t mode, uin
             }
             s.part[t] = acc;
             __syncthreads();
-            if (t < RS_NR) {
+            if (t < nr) {
                 uint32_t v = 0;
 #pragma unroll
                 for (int k = 0; k < 8; ++k)
@@ -508,7 +510,7 @@ __device__ void dec1_body(Dec1Smem &s, const RsCorrParams &P, uint32_t mode, uin
             uint32_t p;
             if (mode == 1u) {
                 /* magnitude q (ascending location) into slot q (quirks Q1/Q2);
-                 * slots past the codeword: parity when < size + 32 (Q4), else dropped */
+                 * slots past the codeword: parity when < size + nr (Q4), else dropped */
                 p = s.pos[t];
             } else {
                 p = (uint32_t)((int32_t)s.locs[t] - pad);
@@ -582,7 +584,14 @@ __global__ __launch_bounds__(S1_WG) void rs_dec1_k(const RsDevTables *__restrict
 extern "C" hipError_t rsk_encode1(const RsDevTables *tab, const uint8_t *data, uint8_t *parity, uint32_t size,
                                   uint32_t *flag, uint32_t seq, hipStream_t stream)
 {
-    RS_LAUNCH(rs_enc1_k, dim3(1), dim3(S1_WG), 0, stream, tab, data, parity, size, flag, seq);
+    RS_LAUNCH(rs_enc1_k, dim3(1), dim3(S1_WG), 0, stream, tab, data, parity, size, flag, seq, (uint32_t)RS_NR);
+    return hipGetLastError();
+}
+
+extern "C" hipError_t rsk_encode1_nr(const RsDevTables *tab, const uint8_t *data, uint8_t *parity, uint32_t size,
+                                     uint32_t npar, uint32_t *flag, uint32_t seq, hipStream_t stream)
+{
+    RS_LAUNCH(rs_enc1_k, dim3(1), dim3(S1_WG), 0, stream, tab, data, parity, size, flag, seq, npar);
     return hipGetLastError();
 }
 
@@ -653,16 +662,16 @@ __global__ __launch_bounds__(S1_WG) void rs_serve_k(const RsDevTables *__restric
         }
         __syncthreads();
         const uint32_t seq = cmd[0], op = cmd[1], size = cmd[2], mode = cmd[3];
-        if ((op != RS_SRV_ENCODE && op != RS_SRV_DECODE) || size == 0u || size > 223u)
+        if ((op != RS_SRV_ENCODE && op != RS_SRV_DECODE) || size == 0u || size > RS_NN - P.nr)
             break; /* uniform: idle, lifetime, RS_SRV_STOP; a malformed request also ends the
                     * launch (the host sees it unserved) */
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, ""); /* this wave's loads of the payload: after the request */
         if (op == RS_SRV_ENCODE) {
-            enc1_body(s.g, reinterpret_cast<uint32_t(*)[8]>(s.part), T, zc + ZC_DATA, zc + ZC_PAR, size);
+            enc1_body(s.g, reinterpret_cast<uint32_t(*)[8]>(s.part), T, zc + ZC_DATA, zc + ZC_PAR, size, P.nr);
         } else {
             RsCorrParams Q = P;
             Q.size = size;
-            Q.pad = (int32_t)(RS_NN - RS_NR - size);
+            Q.pad = (int32_t)(RS_NN - P.nr - size);
             dec1_body(s, Q, mode, zc + ZC_DATA, zc + ZC_PAR, nullptr, reinterpret_cast<const uint32_t *>(zc + ZC_POS),
                       zc + ZC_CNT, 4u, reinterpret_cast<const uint16_t *>(zc + ZC_EXT), zc + ZC_OK, zc + ZC_COR);
         }

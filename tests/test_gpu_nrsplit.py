@@ -182,6 +182,8 @@ def test_every_size_vs_oracle(torch_cuda, params, monkeypatch):
         torch.cuda.synchronize()
         got = dev.cpu().numpy()[off:off + n * w].reshape(n, w)
         assert (got[:, size:size + nr] == want).all(), size
+        for c in range(0, n, 32):  # single calls (rs_enc1_k with the code's encq rows)
+            assert (h.encode(data[c]) == want[c]).all(), (size, c)
         cw = _channel(rng, data, want, nr, t)
         rows[:, :size + nr] = cw
         dev = torch.from_numpy(buf).cuda()
