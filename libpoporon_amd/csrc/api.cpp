@@ -1281,13 +1281,15 @@ static bool launch_encode(poporon_t *h, const uint8_t *d_data, size_t ds, uint8_
  * byte-symbol code of npar roots (h->nrsplit), its list on the general kernel */
 static bool launch_split(poporon_t *h, const RsCorrParams &prm, const RsSplitWs &ws, uint8_t *d_data, size_t ds,
                          uint8_t *d_par, size_t ps, size_t size, size_t count, uint8_t *ok, uint8_t *corrected,
-                         hipStream_t s, uint32_t npar = RS_NR)
+                         hipStream_t s, uint32_t npar = RS_NR, const uint16_t *ext = nullptr, size_t ext_stride = 0)
 {
     GpuCtx &g = h->gpu;
     const bool nr = npar < RS_NR;
     {
         KernelTimer t(g, POPORON_AMD_KERNEL_REMAINDER, s);
-        if (nr)
+        if (ext) /* external log-form syndromes (src/decode.c:446-464): converted, refusals to the list */
+            HIP_OK(rsk_ext_syn(g.tab, ext, ext_stride, count, npar, ws.syn, ws.list, ws.nlist, s));
+        else if (nr)
             HIP_OK(rsk_syndrome_reset_nr(g.tab, d_data, ds, d_par, ps, (uint32_t)size, count, ws.syn, ws.nlist, npar,
                                          g.num_cu, s));
         else
@@ -1328,11 +1330,11 @@ static bool launch_split(poporon_t *h, const RsCorrParams &prm, const RsSplitWs 
             RsGenParams gp = h->gen;
             gp.size = (uint32_t)size;
             gp.pad = prm.pad;
-            HIP_OK(rsg_decode_list(g.gtab, &gp, d_data, ds, d_par, ps, count, ws.list, ws.nlist, nullptr, 0, nullptr,
-                                   ok, corrected, g.num_cu, s));
+            HIP_OK(rsg_decode_list(g.gtab, &gp, d_data, ds, d_par, ps, count, ws.list, ws.nlist, ext, ext_stride,
+                                   nullptr, 0, nullptr, ok, corrected, g.num_cu, s));
         } else {
-            HIP_OK(rsk_wave(g.tab, &prm, d_data, ds, d_par, ps, count, ws.list, ws.nlist, ws.syn, nullptr, 0, nullptr,
-                            nullptr, 0, nullptr, ok, corrected, g.num_cu, s));
+            HIP_OK(rsk_wave(g.tab, &prm, d_data, ds, d_par, ps, count, ws.list, ws.nlist, ext ? nullptr : ws.syn, ext,
+                            ext_stride, nullptr, nullptr, 0, nullptr, ok, corrected, g.num_cu, s));
         }
         t.done();
     }
@@ -1366,7 +1368,7 @@ static bool launch_decode(poporon_t *h, uint8_t *d_data, size_t ds, uint8_t *d_p
         t.done();
         return true;
     }
-    if (h->nrsplit && !ext_syn && !pos8 && !pos32 && h->corr.vfast && !h->corr.force_verify &&
+    if (h->nrsplit && !pos8 && !pos32 && h->corr.vfast && !h->corr.force_verify &&
         (h->decode_path == 1 || h->decode_path == 0)) {
         /* a byte-symbol code of fewer than 32 roots, errors only: the split
          * kernels with npar = num_roots, the list on the general kernel --
@@ -1385,7 +1387,8 @@ static bool launch_decode(poporon_t *h, uint8_t *d_data, size_t ds, uint8_t *d_p
             rem_cap = h->gpu.rem_cap;
         }
         const RsSplitWs ws = rs_ws_carve(rem, rem_cap ? rem_cap : count);
-        if (!launch_split(h, prm, ws, d_data, ds, d_par, ps, size, count, ok, corrected, s, h->rs->num_roots))
+        if (!launch_split(h, prm, ws, d_data, ds, d_par, ps, size, count, ok, corrected, s, h->rs->num_roots, ext_syn,
+                          ext_stride))
             return false;
         return !shared || rem_release(h->gpu, s);
     }
@@ -1435,8 +1438,8 @@ static bool launch_decode(poporon_t *h, uint8_t *d_data, size_t ds, uint8_t *d_p
             RsGenParams gp = h->gen;
             gp.size = (uint32_t)size;
             gp.pad = prm.pad;
-            HIP_OK(rsg_decode_list(g.gtab, &gp, d_data, ds, d_par, ps, count, ws.list, ws.nlist, pos8, pos_stride, cnt,
-                                   ok, corrected, g.num_cu, s));
+            HIP_OK(rsg_decode_list(g.gtab, &gp, d_data, ds, d_par, ps, count, ws.list, ws.nlist, nullptr, 0, pos8,
+                                   pos_stride, cnt, ok, corrected, g.num_cu, s));
             t.done();
         }
         {
@@ -1475,6 +1478,25 @@ static bool launch_decode(poporon_t *h, uint8_t *d_data, size_t ds, uint8_t *d_p
                         pos8, pos32, pos_stride, cnt, ok, corrected, h->gpu.num_cu, s));
         t.done();
         return true;
+    }
+    /* external syndromes of a large batch: the split kernels from converted
+     * syndromes, refusals and what they hand on to rs_wave_k (which reads
+     * the external syndromes itself) */
+    const bool xsplit = ext_syn && !pos8 && !pos32 && prm.vfast && !prm.force_verify && h->decode_path != 2 &&
+                        (h->decode_path == 1 || count >= SPLIT_MIN_COUNT);
+    if (xsplit) {
+        const bool own = !rem;
+        if (own) {
+            if (!ensure_rem(h, count) || !rem_acquire(h->gpu, s))
+                return false;
+            rem = h->gpu.rem;
+            rem_cap = h->gpu.rem_cap;
+        }
+        const RsSplitWs ws = rs_ws_carve(rem, rem_cap ? rem_cap : count);
+        if (!launch_split(h, prm, ws, d_data, ds, d_par, ps, size, count, ok, corrected, s, RS_NR, ext_syn,
+                          ext_stride))
+            return false;
+        return !own || rem_release(h->gpu, s);
     }
     const bool shared = !rem && !ext_syn; /* the handle's workspace */
     if (shared) {

@@ -238,6 +238,11 @@ hipError_t rsk_syn_log(const RsDevTables *tab, const uint8_t *syn, size_t count,
 /* flag[c] = remainder of codeword c is nonzero */
 hipError_t rsk_check(const RsDevTables *tab, const uint8_t *data, size_t dstride, const uint8_t *parity, size_t pstride,
                      uint32_t size, size_t count, uint8_t *flag, int num_cu, hipStream_t stream);
+/* external log-form syndromes (npar per codeword, ext_stride apart) -> the
+ * split decode's poly syndromes (syn); refused codewords (a value > 255) put
+ * on the list with zero syndromes; zeroes nlist[0..1] first */
+hipError_t rsk_ext_syn(const RsDevTables *tab, const uint16_t *ext, size_t ext_stride, size_t count, uint32_t npar,
+                       uint8_t *syn, uint32_t *list, uint32_t *nlist, hipStream_t stream);
 /* the same two for a byte-symbol code of npar < 32 roots (tables of
  * build_tables_nr): log-form syndromes S_0..S_(npar-1), the remainder flag */
 hipError_t rsk_syn_log_nr(const RsDevTables *tab, const uint8_t *syn, size_t count, uint16_t *out, size_t stride,

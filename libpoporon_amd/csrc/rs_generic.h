@@ -41,12 +41,12 @@ hipError_t rsg_decode(const RsGenTables *tab, const RsGenParams *prm, uint8_t *d
                       const uint32_t *pos32, size_t pos_stride, const uint8_t *cnt, uint8_t *ok, uint8_t *corrected,
                       int num_cu, hipStream_t stream);
 /* decode of the codewords list[0 .. *list_n) (the split decode's hand-off for
- * codes of fewer than 32 roots; length read on the device): errors only
- * (pos8 NULL) or with u8 erasure slots */
+ * codes of fewer than 32 roots; length read on the device): errors only,
+ * external syndromes (ext) or u8 erasure slots (pos8) */
 hipError_t rsg_decode_list(const RsGenTables *tab, const RsGenParams *prm, uint8_t *data, size_t dstride,
                            uint8_t *parity, size_t pstride, size_t count, const uint32_t *list, const uint32_t *list_n,
-                           const uint8_t *pos8, size_t pos_stride, const uint8_t *cnt, uint8_t *ok,
-                           uint8_t *corrected, int num_cu, hipStream_t stream);
+                           const uint16_t *ext, size_t ext_stride, const uint8_t *pos8, size_t pos_stride,
+                           const uint8_t *cnt, uint8_t *ok, uint8_t *corrected, int num_cu, hipStream_t stream);
 
 /* dirty[c] = any syndrome nonzero (may be NULL); syn (may be NULL): the
  * nroots log-form syndromes of codeword c at syn[c*syn_stride ..] */

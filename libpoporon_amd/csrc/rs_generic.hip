@@ -466,12 +466,13 @@ extern "C" hipError_t rsg_decode(const RsGenTables *tab, const RsGenParams *prm,
 
 /* decode of the codewords list[0 .. *list_n) (at most count; the grid is
  * sized for a list of up to 1/16 of the batch and loops past it): errors
- * only, or with u8 erasure slots (pos8 / pos_stride / cnt) */
+ * only, with external log-form syndromes (ext), or with u8 erasure slots
+ * (pos8 / pos_stride / cnt) */
 extern "C" hipError_t rsg_decode_list(const RsGenTables *tab, const RsGenParams *prm, uint8_t *data, size_t dstride,
                                       uint8_t *parity, size_t pstride, size_t count, const uint32_t *list,
-                                      const uint32_t *list_n, const uint8_t *pos8, size_t pos_stride,
-                                      const uint8_t *cnt, uint8_t *ok, uint8_t *corrected, int num_cu,
-                                      hipStream_t stream)
+                                      const uint32_t *list_n, const uint16_t *ext, size_t ext_stride,
+                                      const uint8_t *pos8, size_t pos_stride, const uint8_t *cnt, uint8_t *ok,
+                                      uint8_t *corrected, int num_cu, hipStream_t stream)
 {
     if (count == 0)
         return hipSuccess;
@@ -479,8 +480,8 @@ extern "C" hipError_t rsg_decode_list(const RsGenTables *tab, const RsGenParams 
     size_t lds;
     g_shape(*prm, 7, wg, lds);
     RS_LAUNCH(rsg_decode_k<uint8_t>, g_grid((count + 15) / 16, wg, num_cu, lds), dim3(wg), lds, stream, tab, *prm,
-              data, dstride, parity, pstride, count, (const uint16_t *)nullptr, (size_t)0, pos8, pos_stride, cnt, ok,
-              corrected, list, list_n);
+              data, dstride, parity, pstride, count, ext, ext_stride, pos8, pos_stride, cnt, ok, corrected, list,
+              list_n);
     return hipGetLastError();
 }
 

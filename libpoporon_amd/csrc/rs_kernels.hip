@@ -826,6 +826,59 @@ extern "C" hipError_t rsk_syn_log_nr(const RsDevTables *tab, const uint8_t *syn,
     return hipGetLastError();
 }
 
+/* External log-form syndromes (the config's "syndrome" branch, src/decode.c:
+ * 446-464) -> the split decode's poly-form syndromes (32 B per codeword,
+ * zeros past npar).  A value above 255 (out of table in the reference) makes
+ * the codeword the list's: its syndromes are written as zeros (the split
+ * kernels pass it by as clean) and the list kernel, reading the external
+ * syndromes itself, refuses it (ok 0, corrected 0).  *nlist must be 0. */
+__global__ __launch_bounds__(256) void rs_ext_syn_k(const RsDevTables *__restrict__ T, const uint16_t *__restrict__ ext,
+                                                    size_t ext_stride, size_t count, uint32_t npar,
+                                                    uint8_t *__restrict__ syn, uint32_t *__restrict__ list,
+                                                    uint32_t *__restrict__ nlist)
+{
+    __shared__ uint8_t ex[256];
+    ex[threadIdx.x] = T->exp2[threadIdx.x];
+    __syncthreads();
+    const size_t cw = (size_t)blockIdx.x * 256u + threadIdx.x;
+    if (cw >= count)
+        return;
+    const uint16_t *e = ext + cw * ext_stride;
+    uint32_t w[RS_NR / 4] = {0, 0, 0, 0, 0, 0, 0, 0};
+    bool bad = false;
+#pragma unroll
+    for (uint32_t i = 0; i < RS_NR; ++i) {
+        if (i < npar) { /* uniform */
+            const uint32_t v = e[i];
+            bad |= v > 255u;
+            w[i >> 2] |= (v >= 255u ? 0u : (uint32_t)ex[v]) << (8u * (i & 3u));
+        }
+    }
+    if (bad) {
+#pragma unroll
+        for (int k = 0; k < RS_NR / 4; ++k)
+            w[k] = 0;
+        list[atomicAdd(nlist, 1u)] = (uint32_t)cw;
+    }
+    uint4 *o = reinterpret_cast<uint4 *>(syn + cw * RS_NR);
+    o[0] = make_uint4(w[0], w[1], w[2], w[3]);
+    o[1] = make_uint4(w[4], w[5], w[6], w[7]);
+}
+
+extern "C" hipError_t rsk_ext_syn(const RsDevTables *tab, const uint16_t *ext, size_t ext_stride, size_t count,
+                                  uint32_t npar, uint8_t *syn, uint32_t *list, uint32_t *nlist, hipStream_t stream)
+{
+    const hipError_t me = hipMemsetAsync(nlist, 0, 2 * sizeof(uint32_t), stream);
+    if (me != hipSuccess)
+        return me;
+    if (count == 0)
+        return hipSuccess;
+    const size_t blocks = (count + 255) / 256;
+    RS_LAUNCH(rs_ext_syn_k, dim3((uint32_t)blocks), dim3(256), 0, stream, tab, ext, ext_stride, count, npar, syn, list,
+              nlist);
+    return hipGetLastError();
+}
+
 extern "C" hipError_t rsk_check(const RsDevTables *tab, const uint8_t *data, size_t dstride, const uint8_t *parity,
                                 size_t pstride, uint32_t size, size_t count, uint8_t *flag, int num_cu,
                                 hipStream_t stream)

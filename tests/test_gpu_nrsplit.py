@@ -335,3 +335,61 @@ def test_nrsplit_check_and_syndromes_vs_oracle(torch_cuda, params):
         for c in range(n):
             f, want = o.syndrome(cw[c, :size], cw[c, size:])
             assert bool(dirty[c]) == f and bool(nz[c]) == f and (got_syn[c] == want).all(), (size, c)
+
+
+@pytest.mark.parametrize("params,path", [((8, 0x11D, 1, 1, 32), "split"), ((8, 0x11D, 1, 1, 32), None),
+                                         ((8, 0x11D, 1, 1, 16), None), ((8, 0x187, 5, 1, 31), None),
+                                         ((8, 0x11D, 0, 1, 2), None), ((8, 0x171, 1, 11, 10), "split")])
+def test_external_syndrome_batches_vs_oracle(torch_cuda, params, path, monkeypatch):
+    """poporon_decode_batch_syndrome_device on the split kernels
+    (rsk_ext_syn converts the log-form syndromes; a value > 255 refuses its
+    codeword through the list): the received word's own syndromes, random
+    syndromes, all-255 rows (clean) and rows holding a value > 255, against
+    the oracle's decode with the same external syndromes (src/decode.c:446-464).
+    RS(255,223) with the override and at 20,000 codewords (the default's split
+    threshold is 16,384); fewer-roots codes at every count."""
+    from oracle import Oracle
+    torch = torch_cuda
+    if path:
+        monkeypatch.setenv("POPORON_AMD_DECODE_PATH", path)
+    m, poly, fcr, prim, nr = params
+    o, h = Oracle(*params), P.Poporon(*params)
+    rng = np.random.default_rng(nr * 31 + prim)
+    s = torch.cuda.current_stream().cuda_stream
+    n = 20000 if (nr == 32 and path is None) else 3000
+    nchk = 3000  # rows checked against the oracle; the rest by the round trip
+    for size in (255 - nr, 60):
+        data = rng.integers(0, 256, (n, size), dtype=np.uint8)
+        clean = np.concatenate([data, o.encode_batch(data)], 1)
+        cw = _channel(rng, data, clean[:, size:].copy(), nr, nr // 2)
+        syn = np.zeros((n, nr), np.uint16)
+        for c in range(n):
+            kind = c % 5 if c < nchk else 0
+            if kind in (0, 1):
+                syn[c] = o.syndrome(cw[c, :size], cw[c, size:])[1]
+            elif kind == 2:
+                syn[c] = rng.integers(0, 256, nr)
+            elif kind == 3:
+                syn[c] = 255
+            else:
+                syn[c] = o.syndrome(cw[c, :size], cw[c, size:])[1]
+                syn[c, rng.integers(0, nr)] = int(rng.integers(256, 65536))
+        dev = torch.from_numpy(cw).cuda()
+        sy = torch.from_numpy(syn.astype(np.int16)).cuda()
+        ok = torch.full((n,), 7, dtype=torch.uint8, device="cuda")
+        cor = torch.full((n,), 7, dtype=torch.uint8, device="cuda")
+        b, w = dev.data_ptr(), size + nr
+        h.timing(True)
+        h.decode_batch_syndrome_device(b, w, b + size, w, size, n, sy.data_ptr(), nr, ok.data_ptr(), cor.data_ptr(), s)
+        torch.cuda.synchronize()
+        assert _bm_launches(h) > 0, "split kernels did not run"
+        h.timing(False)
+        got, gok, gcor = dev.cpu().numpy(), ok.cpu().numpy(), cor.cpu().numpy()
+        for c in range(nchk):
+            if (syn[c] > 255).any():  # out of the reference's tables (no defined result): refused, untouched
+                wok, wn, wd, wp = False, 0, cw[c, :size], cw[c, size:]
+            else:
+                wok, wn, wd, wp = o.decode(cw[c, :size], cw[c, size:], ext_syn=syn[c])
+            assert gok[c] == wok and gcor[c] == wn, (size, c, c % 5)
+            assert (got[c, :size] == wd).all() and (got[c, size:] == wp).all(), (size, c, c % 5)
+        assert (gok[nchk:] == 1).all() and (got[nchk:] == clean[nchk:]).all()
