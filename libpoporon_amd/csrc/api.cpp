@@ -176,6 +176,8 @@ struct _poporon_t {
     bool generic;   /* served by the general-parameter kernels (rs_generic.hip) */
     bool lfsr_nr;   /* generic byte-symbol code, num_roots < 32: batch encodes on the LFSR kernel (rsk_encode_nr) */
     bool nrsplit;   /* ... and large error-mode batches decode on the split kernels (params_nrsplit) */
+    int gen_path;   /* general kernels: 0 by batch size, 1 one codeword per lane (rsg_*), 2 one per wave
+                       (rsgw_*); POPORON_AMD_GENERIC=lane|wave */
     RsDevTables host_tab;
     RsCorrParams corr;
     RsGenTables gen_tab;
@@ -568,6 +570,26 @@ static void build_generic(poporon_t *h)
     }
     for (uint32_t i = 0; i <= rs->num_roots; i++)
         t.gen[i] = (uint8_t)rs->generator_polynomial[i];
+    /* encq: the register after each byte of the message 1, 0, 0, ... -- the
+     * steps of src/encode.c:120-143 as rsg_encode_k takes them (the
+     * generator's logs used as they are) */
+    {
+        const uint32_t nr = rs->num_roots;
+        const uint16_t *g = rs->generator_polynomial;
+        memset(t.encq, 0xff, sizeof(t.encq));
+        std::vector<uint8_t> reg(nr, 0);
+        for (uint32_t d = 0; d < nn - nr; d++) {
+            const uint32_t fb = gf->exp2log[(d == 0 ? 1u : 0u) ^ reg[0]];
+            if (fb != nn)
+                for (uint32_t j = 1; j < nr; j++)
+                    reg[j] ^= (uint8_t)gf->log2exp[gf_mod(gf, (uint16_t)(fb + g[nr - j]))];
+            for (uint32_t j = 0; j + 1 < nr; j++)
+                reg[j] = reg[j + 1];
+            reg[nr - 1] = fb != nn ? (uint8_t)gf->log2exp[gf_mod(gf, (uint16_t)(fb + g[0]))] : 0;
+            for (uint32_t j = 0; j < nr; j++)
+                t.encq[d * 256 + j] = reg[j] ? (uint8_t)gf->exp2log[reg[j]] : (uint8_t)0xff;
+        }
+    }
     RsGenParams &p = h->gen;
     memset(&p, 0, sizeof(p));
     p.m = gf->symbol_size;
@@ -793,6 +815,10 @@ EXPORT poporon_t *poporon_create(const poporon_config_t *config)
     h->lfsr_nr = h->generic && params_lfsr_nr(h);
     h->nrsplit = h->lfsr_nr && params_nrsplit(h);
     h->supported = h->fast || h->generic;
+    {
+        const char *gp = getenv("POPORON_AMD_GENERIC");
+        h->gen_path = !gp ? 0 : !strcmp(gp, "lane") ? 1 : !strcmp(gp, "wave") ? 2 : 0;
+    }
     if (h->fast)
         build_tables(h);
     if (h->generic)
@@ -1246,6 +1272,21 @@ static bool rem_release(GpuCtx &g, hipStream_t s)
     return true;
 }
 
+/* general parameters: one codeword per wave (rsgw_*) or per lane (rsg_*).
+ * The wave kernels take single calls and batches below 16,384 codewords of
+ * every code (a few us to ~0.35 ms per call against 20 us to 24 ms), and
+ * large batches of long codes: decode from 127-symbol codewords, encode of
+ * 255-symbol ones.  Large batches of short codes keep one codeword per lane
+ * (65,536 codewords of 2^m - 1 = 63 / 31 / 15: 213 / 84 / 79 us against 242
+ * / 172 / 201 us per decode call; profiles/r05_general_lat_*.log) */
+static bool gen_wave(const poporon_t *h, size_t count, bool encode)
+{
+    if (h->gen_path)
+        return h->gen_path == 2;
+    const uint32_t nn = h->rs->gf->field_size;
+    return count < 16384 || (encode ? nn == 255u : nn >= 127u);
+}
+
 static bool launch_encode(poporon_t *h, const uint8_t *d_data, size_t ds, uint8_t *d_par, size_t ps, size_t size,
                           size_t count, hipStream_t s)
 {
@@ -1264,7 +1305,10 @@ static bool launch_encode(poporon_t *h, const uint8_t *d_data, size_t ds, uint8_
     } else {
         RsGenParams prm = h->gen;
         prm.size = (uint32_t)size;
-        HIP_OK(rsg_encode(h->gpu.gtab, &prm, d_data, ds, d_par, ps, count, h->gpu.num_cu, s));
+        if (gen_wave(h, count, true))
+            HIP_OK(rsgw_encode(h->gpu.gtab, &prm, d_data, ds, d_par, ps, count, h->gpu.num_cu, s));
+        else
+            HIP_OK(rsg_encode(h->gpu.gtab, &prm, d_data, ds, d_par, ps, count, h->gpu.num_cu, s));
     }
     t.done();
     return true;
@@ -1330,8 +1374,12 @@ static bool launch_split(poporon_t *h, const RsCorrParams &prm, const RsSplitWs 
             RsGenParams gp = h->gen;
             gp.size = (uint32_t)size;
             gp.pad = prm.pad;
-            HIP_OK(rsg_decode_list(g.gtab, &gp, d_data, ds, d_par, ps, count, ws.list, ws.nlist, ext, ext_stride,
-                                   nullptr, 0, nullptr, ok, corrected, g.num_cu, s));
+            if (h->gen_path == 1)
+                HIP_OK(rsg_decode_list(g.gtab, &gp, d_data, ds, d_par, ps, count, ws.list, ws.nlist, ext, ext_stride,
+                                       nullptr, 0, nullptr, ok, corrected, g.num_cu, s));
+            else
+                HIP_OK(rsgw_decode(g.gtab, &gp, d_data, ds, d_par, ps, count, ext, ext_stride, nullptr, nullptr, 0,
+                                   nullptr, ok, corrected, ws.list, ws.nlist, g.num_cu, s));
         } else {
             HIP_OK(rsk_wave(g.tab, &prm, d_data, ds, d_par, ps, count, ws.list, ws.nlist, ext ? nullptr : ws.syn, ext,
                             ext_stride, nullptr, nullptr, 0, nullptr, ok, corrected, g.num_cu, s));
@@ -1438,8 +1486,12 @@ static bool launch_decode(poporon_t *h, uint8_t *d_data, size_t ds, uint8_t *d_p
             RsGenParams gp = h->gen;
             gp.size = (uint32_t)size;
             gp.pad = prm.pad;
-            HIP_OK(rsg_decode_list(g.gtab, &gp, d_data, ds, d_par, ps, count, ws.list, ws.nlist, nullptr, 0, pos8,
-                                   pos_stride, cnt, ok, corrected, g.num_cu, s));
+            if (h->gen_path == 1)
+                HIP_OK(rsg_decode_list(g.gtab, &gp, d_data, ds, d_par, ps, count, ws.list, ws.nlist, nullptr, 0, pos8,
+                                       pos_stride, cnt, ok, corrected, g.num_cu, s));
+            else
+                HIP_OK(rsgw_decode(g.gtab, &gp, d_data, ds, d_par, ps, count, nullptr, 0, pos8, nullptr, pos_stride,
+                                   cnt, ok, corrected, ws.list, ws.nlist, g.num_cu, s));
             t.done();
         }
         {
@@ -1454,8 +1506,12 @@ static bool launch_decode(poporon_t *h, uint8_t *d_data, size_t ds, uint8_t *d_p
         prm.size = (uint32_t)size;
         prm.pad = (int32_t)(h->rs->gf->field_size - h->rs->num_roots - size);
         KernelTimer t(h->gpu, POPORON_AMD_KERNEL_CORRECT, s);
-        HIP_OK(rsg_decode(h->gpu.gtab, &prm, d_data, ds, d_par, ps, count, ext_syn, ext_stride, pos8, pos32,
-                          pos_stride, cnt, ok, corrected, h->gpu.num_cu, s));
+        if (gen_wave(h, count, false))
+            HIP_OK(rsgw_decode(h->gpu.gtab, &prm, d_data, ds, d_par, ps, count, ext_syn, ext_stride, pos8, pos32,
+                               pos_stride, cnt, ok, corrected, nullptr, nullptr, h->gpu.num_cu, s));
+        else
+            HIP_OK(rsg_decode(h->gpu.gtab, &prm, d_data, ds, d_par, ps, count, ext_syn, ext_stride, pos8, pos32,
+                              pos_stride, cnt, ok, corrected, h->gpu.num_cu, s));
         t.done();
         return true;
     }

@@ -16,6 +16,9 @@ struct RsGenTables {
     uint8_t alog[256]; /* log2exp: alpha^i for i < nn, alog[nn] = 0 (entries past nn: 0) */
     uint8_t log[256];  /* exp2log: log[0] = nn (entries past nn: nn) */
     uint8_t gen[256];  /* generator, log form, gen[0..nroots] */
+    /* parity of the message 1 followed by d zeros, row d (stride 256), log
+     * form, 0xff: zero (the reference's LFSR, src/encode.c:120-143) */
+    uint8_t encq[255 * 256];
 };
 
 struct RsGenParams {
@@ -28,6 +31,16 @@ struct RsGenParams {
 #ifdef __cplusplus
 extern "C" {
 #endif
+
+/* one codeword per wave (latency: single calls, small batches, lists,
+ * long root counts); same arguments and results as rsg_encode / rsg_decode,
+ * list / list_n as rsg_decode_list */
+hipError_t rsgw_encode(const RsGenTables *tab, const RsGenParams *prm, const uint8_t *data, size_t dstride,
+                       uint8_t *parity, size_t pstride, size_t count, int num_cu, hipStream_t stream);
+hipError_t rsgw_decode(const RsGenTables *tab, const RsGenParams *prm, uint8_t *data, size_t dstride, uint8_t *parity,
+                       size_t pstride, size_t count, const uint16_t *ext, size_t ext_stride, const uint8_t *pos8,
+                       const uint32_t *pos32, size_t pos_stride, const uint8_t *cnt, uint8_t *ok, uint8_t *corrected,
+                       const uint32_t *list, const uint32_t *list_n, int num_cu, hipStream_t stream);
 
 hipError_t rsg_encode(const RsGenTables *tab, const RsGenParams *prm, const uint8_t *data, size_t dstride,
                       uint8_t *parity, size_t pstride, size_t count, int num_cu, hipStream_t stream);

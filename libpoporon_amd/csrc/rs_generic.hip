@@ -409,6 +409,563 @@ __global__ __launch_bounds__(G_WG_MAX) void rsg_check_k(const RsGenTables *__res
     }
 }
 
+
+/* ======================================================================== */
+/* one codeword per wave (rsgw_*): the same steps and integer semantics,     */
+/* the polynomial coefficients, syndromes, Chien points and roots spread     */
+/* over the 64 lanes (index i on lane i % 64, register slot i / 64)          */
+/* ======================================================================== */
+/* The one-codeword-per-lane kernels above run each codeword as one serial
+ * chain of ~size * nroots dependent LDS lookups: ~1 ms for a single call of
+ * RS(255,239)-sized codes, 23 ms for 200 roots.  Here a wave shares the
+ * work of one codeword: syndromes as independent terms (or per-root Horner
+ * where the reference's uint16 exponent truncation makes the multiplier
+ * depend on the operand), BM with coefficient i on lane i % 64 (the
+ * discrepancy by a DPP/permlane XOR reduction, B[i - 1] by a DPP shift),
+ * Chien over all points at once, Omega / Forney / the re-syndrome check
+ * with lanes over their indices, the apply from an LDS copy of the row. */
+#define GW_WG 256
+#define GW_Z 512u   /* log of zero in the sentinel arrays: any sum with it indexes al2's zero part */
+#define GW_AL2 1536 /* al2[x] = alpha^(x mod nn) for x < 2 nn, 0 from there on */
+
+struct GwWave {
+    uint8_t cw[256];    /* the received row [data | parity], raw bytes */
+    uint16_t lr[256];   /* log of each masked byte (GW_Z: zero) */
+    uint8_t S[256];     /* syndromes, log form (nn: zero) */
+    uint16_t sz[256];   /* the same, GW_Z for zero */
+    uint8_t lam[256];   /* locator, log form */
+    uint16_t lamz[256];
+    uint16_t omz[256];  /* Omega, log form, GW_Z for zero */
+    uint8_t roots[256], locs[256], mag[256];
+    uint32_t acc[256];  /* syndrome partial sums / erasure slots / apply deltas */
+};
+
+struct GwSmem {
+    uint8_t alog[256], log[256];
+    uint8_t al2[GW_AL2];
+    GwWave w[GW_WG / 64];
+};
+
+/* lane order within a wave: LDS writes by some lanes, then reads by others */
+__device__ __forceinline__ void gw_sync()
+{
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+/* XOR over the wave, in every lane (permlane swaps across halves and rows,
+ * DPP within a row) */
+__device__ __forceinline__ uint32_t gw_xor(uint32_t v)
+{
+    const auto a = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+    v = a[0] ^ a[1];
+    const auto b = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+    v = b[0] ^ b[1];
+    v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x128, 0xf, 0xf, false); /* row_ror:8 */
+    v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x124, 0xf, 0xf, false); /* row_ror:4 */
+    v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xf, 0xf, false);  /* quad_perm [2,3,0,1] */
+    v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xf, 0xf, false);  /* quad_perm [1,0,3,2] */
+    return v;
+}
+
+/* out[i] = v[i - 1] over the four register slots (index i = lane + 64 q);
+ * out[0] = first.  DPP wave_shr:1, the slot's carry through lane 63 */
+__device__ __forceinline__ void gw_shift(const uint32_t (&v)[4], uint32_t (&out)[4], uint32_t lane, uint32_t first)
+{
+    uint32_t carry = first;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const uint32_t top = (uint32_t)__builtin_amdgcn_readlane((int)v[q], 63);
+        const uint32_t u = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v[q], 0x138, 0xf, 0xf, true);
+        out[q] = lane ? u : carry;
+        carry = top;
+    }
+}
+
+__device__ __forceinline__ void gw_tables(GwSmem &sm, const RsGenTables *__restrict__ T, uint32_t nn)
+{
+    const uint32_t t = threadIdx.x;
+    sm.alog[t] = T->alog[t];
+    sm.log[t] = T->log[t];
+    for (uint32_t x = t; x < GW_AL2; x += GW_WG)
+        sm.al2[x] = x < nn ? T->alog[x] : (x < 2u * nn ? T->alog[x - nn] : (uint8_t)0);
+}
+
+/* syndromes of the row in W.cw / W.lr into W.S / W.sz; true if any is nonzero
+ * (src/decode.c:375-415).  qf: (fcr + nr - 1) prim + nn - 1 < 2^16, so the
+ * reference's Horner step multiplies by the constant alpha^((fcr + i) prim
+ * mod nn) and S_i = sum_b r_b alpha^(s_i (total - 1 - b)): independent terms,
+ * G = 64 / nr lanes per root for short root counts (partial sums XORed in
+ * LDS).  Else the reference's Horner, one root per lane. */
+__device__ bool gw_syndromes(const GwSmem &sm, GwWave &W, const RsGenParams &P, const GMod &mod, uint32_t lane,
+                             bool qf)
+{
+    const uint32_t nr = P.nroots, nn = P.nn, A0 = P.nn, total = P.size + nr;
+    const uint8_t *al2 = sm.al2, *lg = sm.log, *alog = sm.alog;
+    uint32_t sv[4] = {0, 0, 0, 0};
+    if (qf) {
+        const uint32_t G = nr <= 32u ? 64u / nr : 1u;
+        const uint32_t U = nr * G;
+        if (G > 1u) {
+            if (lane < nr)
+                W.acc[lane] = 0;
+            gw_sync();
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const uint32_t u = lane + 64u * q;
+            if (u < U) {
+                const uint32_t i = G > 1u ? u % nr : u, g = G > 1u ? u / nr : 0u;
+                const uint32_t sx = mod((P.fcr + i) * P.prim);
+                const uint32_t sg = mod(sx * G);
+                uint32_t acc = 0;
+                if (g < total) {
+                    uint32_t e = mod(sx * (total - 1u - g));
+                    for (uint32_t b = g; b < total; b += G) {
+                        acc ^= al2[W.lr[b] + e];
+                        e = e >= sg ? e - sg : e + nn - sg;
+                    }
+                }
+                if (G > 1u)
+                    atomicXor(&W.acc[i], acc);
+                else
+                    sv[q] = acc;
+            }
+        }
+        if (G > 1u) {
+            gw_sync();
+            sv[0] = lane < nr ? W.acc[lane] : 0u;
+        }
+    } else {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const uint32_t i = lane + 64u * q;
+            if (i < nr) {
+                const uint32_t step = P.fcr * P.prim + i * P.prim; /* int arithmetic, truncated inside gf_mod */
+                uint32_t v = (uint32_t)W.cw[0] & A0;
+                for (uint32_t b = 1; b < total; ++b) {
+                    const uint32_t in = (uint32_t)W.cw[b] & A0;
+                    v = v ? (in ^ alog[mod((uint32_t)lg[v] + step)]) : in;
+                }
+                sv[q] = v;
+            }
+        }
+    }
+    bool nz = false;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const uint32_t i = lane + 64u * q;
+        if (i < nr) {
+            const uint32_t l = lg[sv[q]];
+            W.S[i] = (uint8_t)l;
+            W.sz[i] = sv[q] ? l : GW_Z;
+            nz |= sv[q] != 0u;
+        }
+    }
+    gw_sync();
+    return __ballot(nz) != 0ull;
+}
+
+/* src/decode.c:17-230 for the row in W (syndromes in W.S / W.sz): erasure
+ * locator, BM, degree, Chien, Omega, Forney, re-syndrome check, apply
+ * (in place in data / parity from W.cw).  Same results as g_correct. */
+template <typename PosT>
+__device__ bool gw_correct(const GwSmem &sm, GwWave &W, const RsGenParams &P, const GMod &mod, uint32_t lane,
+                           uint8_t *data, uint8_t *parity, uint32_t ne, const PosT *pos, bool eras_apply,
+                           uint32_t &corrected)
+{
+    const uint32_t nr = P.nroots, nn = P.nn, A0 = P.nn, size = P.size;
+    const int32_t pad = P.pad;
+    const uint8_t *alog = sm.alog, *lg = sm.log, *al2 = sm.al2;
+    uint32_t lam[4], B[4], Bm[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+        lam[q] = (lane + 64u * q) == 0u ? 1u : 0u;
+
+    /* erasure locator prod (1 + X_l x), src/decode.c:31-47 */
+    if (ne > 0u) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const uint32_t i = lane + 64u * q;
+            if (i < ne)
+                W.acc[i] = (uint32_t)pos[i];
+        }
+        gw_sync();
+        for (uint32_t e = 0; e < ne; ++e) {
+            const uint32_t xl = mod(P.prim * (A0 - 1u - (W.acc[e] + (uint32_t)pad)));
+            gw_shift(lam, Bm, lane, 0u);
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+                if (Bm[q] != 0u)
+                    lam[q] ^= al2[xl + lg[Bm[q]]];
+        }
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+        B[q] = lg[lam[q]];
+
+    /* Berlekamp-Massey, src/decode.c:49-96 */
+    uint32_t L = ne;
+    for (uint32_t r = ne + 1u; r <= nr; ++r) {
+        uint32_t part = 0;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const uint32_t i = lane + 64u * q;
+            if (i < r && lam[q] != 0u) {
+                const uint32_t sv = W.S[r - i - 1u];
+                if (sv != A0)
+                    part ^= al2[lg[lam[q]] + sv];
+            }
+        }
+        const uint32_t disc = lg[gw_xor(part)];
+        if (disc == A0) {
+            gw_shift(B, Bm, lane, A0);
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+                B[q] = Bm[q];
+            continue;
+        }
+        const bool lengthen = 2u * L <= r + ne - 1u;
+        gw_shift(B, Bm, lane, A0);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const uint32_t old = lam[q];
+            if (Bm[q] != A0)
+                lam[q] = old ^ al2[disc + Bm[q]];
+            if (lengthen) {
+                const uint32_t v = (uint32_t)lg[old] + nn - disc;
+                B[q] = old == 0u ? A0 : (v >= nn ? v - nn : v);
+            } else {
+                B[q] = Bm[q];
+            }
+        }
+        if (lengthen)
+            L = r + ne - L;
+    }
+
+    /* locator to log form, degree, src/decode.c:98-110 */
+    uint32_t deg = 0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const uint32_t i = lane + 64u * q;
+        const uint32_t l = lg[lam[q]];
+        const bool valid = i <= nr;
+        if (valid) {
+            W.lam[i] = (uint8_t)l;
+            W.lamz[i] = l == A0 ? GW_Z : l;
+        }
+        const uint64_t m = __ballot(valid && l != A0);
+        if (m)
+            deg = 64u * q + 63u - (uint32_t)__clzll((long long)m);
+    }
+    if (deg == 0u)
+        return false;
+    gw_sync();
+
+    /* Chien search, src/decode.c:112-145: point i = lane + 1 + 64 q; the
+     * first deg roots in ascending order, the padding check on each */
+    {
+        uint32_t acc[4], pm[4], tt[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const uint32_t pt = lane + 1u + 64u * q;
+            pm[q] = pt >= nn ? pt - nn : pt;
+            acc[q] = 1;
+            tt[q] = 0;
+        }
+        for (uint32_t j = 1; j <= deg; ++j) {
+            const uint32_t lz = W.lamz[j];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                tt[q] += pm[q];
+                tt[q] = tt[q] >= nn ? tt[q] - nn : tt[q];
+                acc[q] ^= al2[lz + tt[q]];
+            }
+        }
+        uint32_t base = 0;
+        bool padbad = false;
+        const uint64_t below = (1ull << lane) - 1ull;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const uint32_t pt = lane + 1u + 64u * q;
+            const bool root = pt <= nn && acc[q] == 0u;
+            const uint64_t m = __ballot(root);
+            const uint32_t rank = base + (uint32_t)__popcll(m & below);
+            if (root && rank < deg) {
+                const uint32_t k = mod(pt * P.iprim - 1u);
+                W.roots[rank] = (uint8_t)pt;
+                W.locs[rank] = (uint8_t)k;
+                padbad |= (int32_t)k < pad;
+            }
+            base += (uint32_t)__popcll(m);
+        }
+        if (__ballot(padbad) != 0ull || base < deg)
+            return false;
+    }
+    gw_sync();
+
+    /* Omega = S Lambda mod x^deg, log form, src/decode.c:147-158 */
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const uint32_t i = lane + 64u * q;
+        if (i < deg) {
+            uint32_t acc = 0;
+            for (uint32_t j = 0; j <= i; ++j)
+                acc ^= al2[W.sz[i - j] + W.lamz[j]];
+            W.omz[i] = acc ? lg[acc] : GW_Z;
+        }
+    }
+    gw_sync();
+
+    /* Forney, src/decode.c:159-191 (corrected counts nonzero numerators) */
+    const uint32_t dtop = (deg < nr - 1u ? deg : nr - 1u) & ~1u;
+    uint32_t fixed = 0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const uint32_t jj = lane + 64u * q;
+        uint32_t num = 0;
+        if (jj < deg) {
+            const uint32_t rt = W.roots[jj];
+            const uint32_t rm = rt >= nn ? rt - nn : rt;
+            uint32_t t = 0;
+            for (uint32_t i = 0; i < deg; ++i) {
+                num ^= al2[W.omz[i] + t];
+                t += rm;
+                t = t >= nn ? t - nn : t;
+            }
+            uint32_t mg = 0;
+            if (num != 0u) {
+                const uint32_t num2 = alog[mod((uint32_t)((int32_t)rt * ((int32_t)P.fcr - 1) + (int32_t)A0))];
+                uint32_t den = 0;
+                for (int32_t i = (int32_t)dtop; i >= 0; i -= 2)
+                    den ^= al2[W.lamz[(uint32_t)i + 1u] + mod((uint32_t)i * rt)];
+                mg = alog[mod((uint32_t)lg[num] + lg[num2] + A0 - lg[den])];
+            }
+            W.mag[jj] = (uint8_t)mg;
+        }
+        fixed += (uint32_t)__popcll(__ballot(jj < deg && num != 0u));
+    }
+    corrected = fixed;
+    gw_sync();
+
+    /* re-syndrome check, src/decode.c:193-209 (int16 exponent) */
+    {
+        bool bad = false;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const uint32_t i = lane + 64u * q;
+            if (i < nr) {
+                uint32_t acc = 0;
+                for (uint32_t j = 0; j < deg; ++j) {
+                    const uint32_t mj = W.mag[j];
+                    if (mj == 0u)
+                        continue;
+                    const int32_t kk = (int16_t)(uint16_t)((P.fcr + i) * P.prim * (A0 - (uint32_t)W.locs[j] - 1u));
+                    acc ^= alog[mod((uint32_t)((int32_t)lg[mj] + kk))];
+                }
+                bad |= acc != alog[W.S[i]];
+            }
+        }
+        if (__ballot(bad) != 0ull)
+            return false;
+    }
+
+    /* apply, src/decode.c:211-227, from the row's copy in W.cw */
+    const uint32_t total = size + nr;
+    if (eras_apply) {
+        /* quirk Q1/Q2: magnitude j goes to slot j (repeated slots accumulate);
+         * slots past data[] address parity (p < size + nr) or are dropped */
+        W.acc[lane] = 0;
+        gw_sync();
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const uint32_t jj = lane + 64u * q;
+            if (jj < deg) {
+                const uint32_t p = (uint32_t)pos[jj], mg = W.mag[jj];
+                if (mg != 0u && p < total)
+                    atomicXor(&W.acc[p >> 2], mg << (8u * (p & 3u)));
+            }
+        }
+        gw_sync();
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const uint32_t b = lane + 64u * q;
+            if (b < total) {
+                const uint32_t dl = (W.acc[b >> 2] >> (8u * (b & 3u))) & 0xffu;
+                if (dl != 0u) {
+                    const uint8_t v = (uint8_t)(W.cw[b] ^ dl);
+                    if (b < size)
+                        data[b] = v;
+                    else
+                        parity[b - size] = v;
+                }
+            }
+        }
+        return true;
+    }
+    /* error locations: the reference stops at the first one outside the row
+     * (those before it applied) */
+    uint32_t first_bad = deg;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const uint32_t jj = lane + 64u * q;
+        const int32_t p = (int32_t)W.locs[jj < 256u ? jj : 0u] - pad;
+        const uint64_t m = __ballot(jj < deg && !(p >= 0 && p < (int32_t)total));
+        if (m != 0ull && first_bad == deg)
+            first_bad = 64u * q + (uint32_t)__builtin_ctzll(m);
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const uint32_t jj = lane + 64u * q;
+        if (jj < first_bad) {
+            const uint32_t p = (uint32_t)((int32_t)W.locs[jj] - pad), mg = W.mag[jj];
+            if (mg != 0u) {
+                const uint8_t v = (uint8_t)(W.cw[p] ^ mg);
+                if (p < size)
+                    data[p] = v;
+                else
+                    parity[p - size] = v;
+            }
+        }
+    }
+    return first_bad == deg;
+}
+
+/* Full decode, branch logic of src/decode.c:431-487, one codeword per wave
+ * (rsg_decode_k's modes: ext / erasure slots / errors; list mode) */
+template <typename PosT>
+__global__ __launch_bounds__(GW_WG) void rsgw_decode_k(const RsGenTables *__restrict__ T, RsGenParams P,
+                                                        uint8_t *data, size_t dstride, uint8_t *parity,
+                                                        size_t pstride, size_t count,
+                                                        const uint16_t *__restrict__ ext, size_t ext_stride,
+                                                        const PosT *__restrict__ pos, size_t pos_stride,
+                                                        const uint8_t *__restrict__ cntv, uint8_t *__restrict__ ok,
+                                                        uint8_t *__restrict__ corrected,
+                                                        const uint32_t *__restrict__ list,
+                                                        const uint32_t *__restrict__ list_n)
+{
+    const size_t n = list ? (size_t)*list_n : count;
+    if ((size_t)blockIdx.x * (GW_WG / 64) >= n)
+        return;
+    __shared__ GwSmem sm;
+    const uint32_t t = threadIdx.x, lane = t & 63u, wave = t >> 6;
+    gw_tables(sm, T, P.nn);
+    __syncthreads();
+    GwWave &W = sm.w[wave];
+    const GMod mod{P.nn, P.magic};
+    const uint32_t nr = P.nroots, A0 = P.nn, size = P.size, total = size + nr;
+    const bool qf = (P.fcr + nr - 1u) * P.prim + A0 - 1u < 65536u;
+    for (size_t e = (size_t)blockIdx.x * (GW_WG / 64) + wave; e < n; e += (size_t)gridDim.x * (GW_WG / 64)) {
+        const size_t cw = list ? (size_t)list[e] : e;
+        uint8_t *d = data + cw * dstride;
+        uint8_t *par = parity + cw * pstride;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const uint32_t b = lane + 64u * q;
+            const uint32_t v = b < size ? d[b] : (b < total ? par[b - size] : 0u);
+            const uint32_t m = v & A0;
+            W.cw[b] = (uint8_t)v;
+            W.lr[b] = m ? (uint32_t)sm.log[m] : GW_Z;
+        }
+        uint32_t fixed = 0;
+        bool good;
+        if (ext) {
+            const uint16_t *x = ext + cw * ext_stride;
+            bool bad = false, any = false;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const uint32_t i = lane + 64u * q;
+                if (i < nr) {
+                    const uint32_t v = x[i];
+                    bad |= v > A0;
+                    any |= v != A0;
+                    W.S[i] = (uint8_t)v;
+                    W.sz[i] = v == A0 ? GW_Z : (v & 0xffu);
+                }
+            }
+            bad = __ballot(bad) != 0ull;
+            any = __ballot(any) != 0ull;
+            gw_sync();
+            good = !bad && (!any || gw_correct<PosT>(sm, W, P, mod, lane, d, par, 0u, (const PosT *)nullptr, false,
+                                                      fixed));
+        } else {
+            gw_sync();
+            const bool dirty = gw_syndromes(sm, W, P, mod, lane, qf);
+            if (pos) {
+                const uint32_t ne = cntv[cw];
+                good = !dirty || (ne <= nr && gw_correct<PosT>(sm, W, P, mod, lane, d, par, ne, pos + cw * pos_stride,
+                                                                true, fixed));
+            } else {
+                good = !dirty ||
+                       gw_correct<PosT>(sm, W, P, mod, lane, d, par, 0u, (const PosT *)nullptr, false, fixed);
+            }
+        }
+        if (lane == 0u) {
+            ok[cw] = good ? 1 : 0;
+            if (corrected)
+                corrected[cw] = (uint8_t)fixed;
+        }
+        gw_sync();
+    }
+}
+
+/* Encode, one message per wave: parity = sum_b d_b Q[size - 1 - b], Q[d] the
+ * parity of the message 1 followed by d zeros (RsGenTables::encq, built on
+ * the host by the reference's LFSR, src/encode.c:120-143, which is linear
+ * in the masked message bytes); lane p (and p + 64 ...) owns parity byte p */
+__global__ __launch_bounds__(GW_WG) void rsgw_encode_k(const RsGenTables *__restrict__ T, RsGenParams P,
+                                                        const uint8_t *__restrict__ data, size_t dstride,
+                                                        uint8_t *__restrict__ parity, size_t pstride, size_t count)
+{
+    if ((size_t)blockIdx.x * (GW_WG / 64) >= count)
+        return;
+    __shared__ uint8_t al2[GW_AL2];
+    __shared__ uint8_t lg[256];
+    __shared__ uint16_t lr[GW_WG / 64][256];
+    const uint32_t t = threadIdx.x, lane = t & 63u, wave = t >> 6;
+    const uint32_t nn = P.nn, A0 = P.nn, nr = P.nroots, size = P.size;
+    lg[t] = T->log[t];
+    for (uint32_t x = t; x < GW_AL2; x += GW_WG)
+        al2[x] = x < nn ? T->alog[x] : (x < 2u * nn ? T->alog[x - nn] : (uint8_t)0);
+    __syncthreads();
+    for (size_t e = (size_t)blockIdx.x * (GW_WG / 64) + wave; e < count; e += (size_t)gridDim.x * (GW_WG / 64)) {
+        const uint8_t *d = data + e * dstride;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const uint32_t b = lane + 64u * q;
+            if (b < size) {
+                const uint32_t m = (uint32_t)d[b] & A0;
+                lr[wave][b] = m ? (uint32_t)lg[m] : GW_Z;
+            }
+        }
+        gw_sync();
+        uint32_t acc[4] = {0, 0, 0, 0};
+        for (uint32_t b = 0; b < size; ++b) {
+            const uint32_t l = lr[wave][b];
+            if (l == GW_Z)
+                continue;
+            const uint8_t *row = T->encq + (size_t)(size - 1u - b) * 256u;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const uint32_t p = lane + 64u * q;
+                if (p < nr) {
+                    const uint32_t qe = row[p];
+                    acc[q] ^= qe == 0xffu ? 0u : (uint32_t)al2[l + qe];
+                }
+            }
+        }
+        uint8_t *out = parity + e * pstride;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const uint32_t p = lane + 64u * q;
+            if (p < nr)
+                out[p] = (uint8_t)acc[q];
+        }
+        gw_sync();
+    }
+}
+
 /* ------------------------------------------------------------------------ */
 /* launchers                                                                */
 /* ------------------------------------------------------------------------ */
@@ -496,5 +1053,42 @@ extern "C" hipError_t rsg_check(const RsGenTables *tab, const RsGenParams *prm, 
     g_shape(*prm, 1, wg, lds);
     RS_LAUNCH(rsg_check_k, g_grid(count, wg, num_cu, lds), dim3(wg), lds, stream, tab, *prm, data, dstride,
                        parity, pstride, count, dirty, syn, syn_stride);
+    return hipGetLastError();
+}
+
+/* ---- one codeword per wave ---- */
+static dim3 gw_grid(size_t waves, int num_cu)
+{
+    const size_t need = (waves + GW_WG / 64 - 1) / (GW_WG / 64);
+    const size_t cap = (size_t)(num_cu > 0 ? num_cu : 256) * 8u;
+    return dim3((uint32_t)std::max<size_t>(1, std::min(need, cap)));
+}
+
+extern "C" hipError_t rsgw_encode(const RsGenTables *tab, const RsGenParams *prm, const uint8_t *data, size_t dstride,
+                                  uint8_t *parity, size_t pstride, size_t count, int num_cu, hipStream_t stream)
+{
+    if (count == 0)
+        return hipSuccess;
+    RS_LAUNCH(rsgw_encode_k, gw_grid(count, num_cu), dim3(GW_WG), 0, stream, tab, *prm, data, dstride, parity, pstride,
+              count);
+    return hipGetLastError();
+}
+
+extern "C" hipError_t rsgw_decode(const RsGenTables *tab, const RsGenParams *prm, uint8_t *data, size_t dstride,
+                                  uint8_t *parity, size_t pstride, size_t count, const uint16_t *ext, size_t ext_stride,
+                                  const uint8_t *pos8, const uint32_t *pos32, size_t pos_stride, const uint8_t *cnt,
+                                  uint8_t *ok, uint8_t *corrected, const uint32_t *list, const uint32_t *list_n,
+                                  int num_cu, hipStream_t stream)
+{
+    if (count == 0)
+        return hipSuccess;
+    /* a list: the grid for up to 1/16 of the batch, looping past it */
+    const dim3 grid = gw_grid(list ? (count + 15) / 16 : count, num_cu);
+    if (pos32)
+        RS_LAUNCH(rsgw_decode_k<uint32_t>, grid, dim3(GW_WG), 0, stream, tab, *prm, data, dstride, parity, pstride,
+                  count, ext, ext_stride, pos32, pos_stride, cnt, ok, corrected, list, list_n);
+    else
+        RS_LAUNCH(rsgw_decode_k<uint8_t>, grid, dim3(GW_WG), 0, stream, tab, *prm, data, dstride, parity, pstride,
+                  count, ext, ext_stride, pos8, pos_stride, cnt, ok, corrected, list, list_n);
     return hipGetLastError();
 }

@@ -1,0 +1,146 @@
+"""General-parameter kernels, one codeword per wave (rs_generic.hip
+rsgw_encode_k / rsgw_decode_k) and one per lane (rsg_*), against the oracle
+on every parameter set of the reference's own tests
+(tests/golden/rs_params_golden.npz): 2..8-bit symbols, 2..200 roots, fcr 0..2000,
+prim 1..37 -- including the sets whose exponents pass 2^16 (the syndromes'
+Horner path) and those the reference itself fails at t errors.
+
+Modes: encode (batch and single call), errors-only decode with 0 .. t + 2
+errors, erasure decode with u8 slots (batch) and u32 slots (single call
+through the erasure object, stale slots past the count included), external
+syndromes (the row's own, random, all-zero and out-of-table values).
+POPORON_AMD_GENERIC=wave|lane selects the kernel family (read at
+poporon_create)."""
+import os
+
+import numpy as np
+import pytest
+
+import libpoporon_amd as P
+
+pytestmark = pytest.mark.gpu
+
+_PARAMS = [tuple(int(x) for x in p) for p in
+           np.load(os.path.join(os.path.dirname(__file__), "golden", "rs_params_golden.npz"))["params"]]
+
+
+@pytest.fixture(scope="module")
+def torch_cuda():
+    import torch
+    assert torch.cuda.is_available()
+    return torch
+
+
+def _rows(rng, o, n, size, nn):
+    data = rng.integers(0, 256, (n, size), dtype=np.uint8)  # raw bytes: the codec masks to m bits
+    return data, o.encode_batch(data)
+
+
+@pytest.mark.parametrize("path", ["wave", "lane"])
+@pytest.mark.parametrize("params", _PARAMS)
+def test_generic_paths_vs_oracle(params, path, monkeypatch):
+    from oracle import Oracle
+    monkeypatch.setenv("POPORON_AMD_GENERIC", path)
+    m, poly, fcr, prim, nr = params
+    o, h = Oracle(*params), P.Poporon(*params)
+    assert h.supported
+    nn = (1 << m) - 1
+    k = nn - nr
+    t = nr // 2
+    rng = np.random.default_rng(sum(params) + (path == "lane"))
+    n = 300 if nr < 100 else 120
+    for size in sorted({k, max(1, k // 2), 1}):
+        data, par = _rows(rng, o, n, size, nn)
+        assert (h.encode_batch(data) == par).all(), size
+        for c in range(0, n, 97):
+            assert (h.encode(data[c]) == par[c]).all(), (size, c)
+        # errors
+        cw = np.concatenate([data, par], 1)
+        for c in range(n):
+            ne = min(c % (t + 3), size + nr)
+            pos = rng.permutation(size + nr)[:ne]
+            cw[c, pos] ^= rng.integers(1, nn + 1, ne).astype(np.uint8)
+        ook, ocor, od, op = o.decode_batch(cw[:, :size], cw[:, size:])
+        ok, cor, d, p = h.decode_batch(cw[:, :size], cw[:, size:])
+        assert (ok == ook).all() and (cor == ocor).all(), size
+        assert (d == od).all() and (p == op).all(), size
+        for c in range(0, n, 61):
+            sok, sn, sd, sp = h.decode(cw[c, :size], cw[c, size:])
+            assert sok == bool(ook[c]) and sn == ocor[c] and (sd == od[c]).all() and (sp == op[c]).all(), (size, c)
+        # erasures (+ errors): u8 slots, stale slots past the count
+        cw = np.concatenate([data, par], 1)
+        slots = np.zeros((n, nr), np.uint32)
+        cnts = np.zeros(n, np.uint32)
+        for c in range(n):
+            e = int(rng.integers(0, nr + 1))
+            extra = int(rng.integers(0, max(1, (nr - e) // 2 + 2)))
+            perm = rng.permutation(size + nr)
+            pos = perm[:min(e, size + nr)]
+            slots[c, :len(pos)] = pos
+            slots[c, len(pos):] = rng.integers(0, size + nr, nr - len(pos))
+            cnts[c] = len(pos)
+            cw[c, pos] ^= rng.integers(0, nn + 1, len(pos)).astype(np.uint8)
+            ex = perm[len(pos):len(pos) + extra]
+            cw[c, ex] ^= rng.integers(1, nn + 1, len(ex)).astype(np.uint8)
+        ook, ocor, od, op = o.decode_batch(cw[:, :size], cw[:, size:], slots, cnts)
+        ok, cor, d, p = h.decode_batch(cw[:, :size], cw[:, size:], slots.astype(np.uint8), cnts.astype(np.uint8))
+        assert (ok == ook).all() and (cor == ocor).all(), ("era", size)
+        assert (d == od).all() and (p == op).all(), ("era", size)
+        er = P.Erasure(nr, nr)
+        he = P.Poporon(m, poly, fcr, prim, nr, erasure=er)
+        for c in range(0, n, 53):
+            er.set(slots[c])  # the stale slots past the count stay in the object, as in the reference
+            er.set(slots[c][:cnts[c]])
+            sok, sn, sd, sp = he.decode(cw[c, :size], cw[c, size:])
+            assert sok == bool(ook[c]) and sn == ocor[c] and (sd == od[c]).all() and (sp == op[c]).all(), c
+        he.close()
+    h.close()
+
+
+@pytest.mark.parametrize("path", ["wave", "lane"])
+@pytest.mark.parametrize("params", [(8, 0x11D, 1, 1, 100), (8, 0x187, 5, 7, 48), (4, 0x13, 1, 2, 8),
+                                    (8, 0x11D, 2000, 37, 32), (6, 0x43, 1, 1, 10)])
+def test_generic_external_syndromes_vs_oracle(torch_cuda, params, path, monkeypatch):
+    from oracle import Oracle
+    torch = torch_cuda
+    monkeypatch.setenv("POPORON_AMD_GENERIC", path)
+    m, poly, fcr, prim, nr = params
+    o, h = Oracle(*params), P.Poporon(*params)
+    nn = (1 << m) - 1
+    k = nn - nr
+    rng = np.random.default_rng(nr + 3)
+    n = 200
+    data, par = _rows(rng, o, n, k, nn)
+    cw = np.concatenate([data, par], 1)
+    syn = np.zeros((n, nr), np.uint16)
+    for c in range(n):
+        ne = c % (nr // 2 + 2)
+        pos = rng.permutation(nn)[:ne]
+        cw[c, pos] ^= rng.integers(1, nn + 1, ne).astype(np.uint8)
+        kind = c % 4
+        if kind == 0:
+            syn[c] = o.syndrome(cw[c, :k], cw[c, k:])[1]
+        elif kind == 1:
+            syn[c] = rng.integers(0, nn + 1, nr)
+        elif kind == 2:
+            syn[c] = nn
+        else:
+            syn[c] = o.syndrome(cw[c, :k], cw[c, k:])[1]
+            syn[c, rng.integers(0, nr)] = nn + 1 + int(rng.integers(0, 300))
+    dev = torch.from_numpy(cw.copy()).cuda()
+    sy = torch.from_numpy(syn.astype(np.int16)).cuda()
+    ok = torch.full((n,), 7, dtype=torch.uint8, device="cuda")
+    cor = torch.full((n,), 7, dtype=torch.uint8, device="cuda")
+    s = torch.cuda.current_stream().cuda_stream
+    b = dev.data_ptr()
+    h.decode_batch_syndrome_device(b, nn, b + k, nn, k, n, sy.data_ptr(), nr, ok.data_ptr(), cor.data_ptr(), s)
+    torch.cuda.synchronize()
+    got, gok, gcor = dev.cpu().numpy(), ok.cpu().numpy(), cor.cpu().numpy()
+    for c in range(n):
+        if (syn[c] > nn).any():  # out of the reference's tables: refused, untouched
+            wok, wn, wd, wp = False, 0, cw[c, :k], cw[c, k:]
+        else:
+            wok, wn, wd, wp = o.decode(cw[c, :k], cw[c, k:], ext_syn=syn[c])
+        assert gok[c] == wok and gcor[c] == wn, (c, c % 4)
+        assert (got[c, :k] == wd).all() and (got[c, k:] == wp).all(), (c, c % 4)
+    h.close()
