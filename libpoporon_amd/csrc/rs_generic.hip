@@ -436,6 +436,8 @@ struct GwWave {
     uint8_t lam[256];   /* locator, log form */
     uint16_t lamz[256];
     uint16_t omz[256];  /* Omega, log form, GW_Z for zero */
+    uint16_t lgm[256];  /* per root: log of its magnitude (0xffff: zero) ... */
+    uint16_t lx[256];   /* ... and nn - 1 - its location (the re-syndrome check's factor) */
     uint8_t roots[256], locs[256], mag[256];
     uint32_t acc[256];  /* syndrome partial sums / erasure slots / apply deltas */
 };
@@ -512,27 +514,34 @@ __device__ bool gw_syndromes(const GwSmem &sm, GwWave &W, const RsGenParams &P, 
                 W.acc[lane] = 0;
             gw_sync();
         }
+        /* G > 1: one unit per lane (q = 0); G = 1: units lane + 64 q, all over
+         * every byte -- one broadcast read of the byte's log for all of them */
+        const uint32_t g = G > 1u ? lane / nr : 0u;
+        const uint32_t nq = (U + 63u) / 64u; /* register slots in use (uniform) */
+        uint32_t e[4], sg[4];
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
             const uint32_t u = lane + 64u * q;
-            if (u < U) {
-                const uint32_t i = G > 1u ? u % nr : u, g = G > 1u ? u / nr : 0u;
-                const uint32_t sx = mod((P.fcr + i) * P.prim);
-                const uint32_t sg = mod(sx * G);
-                uint32_t acc = 0;
-                if (g < total) {
-                    uint32_t e = mod(sx * (total - 1u - g));
-                    for (uint32_t b = g; b < total; b += G) {
-                        acc ^= al2[W.lr[b] + e];
-                        e = e >= sg ? e - sg : e + nn - sg;
+            const uint32_t i = G > 1u ? lane % nr : u;
+            const uint32_t sx = mod((P.fcr + i) * P.prim);
+            sg[q] = mod(sx * G);
+            e[q] = g < total ? mod(sx * (total - 1u - g)) : 0u;
+        }
+        if (lane + 64u * 0u < U) {
+#pragma unroll 4
+            for (uint32_t b = g; b < total; b += G) {
+                const uint32_t l = W.lr[b];
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    if ((uint32_t)q < nq && lane + 64u * q < U) { /* q > 0 only for G = 1: the same b for every q */
+                        sv[q] ^= al2[l + e[q]];
+                        e[q] = e[q] >= sg[q] ? e[q] - sg[q] : e[q] + nn - sg[q];
                     }
                 }
-                if (G > 1u)
-                    atomicXor(&W.acc[i], acc);
-                else
-                    sv[q] = acc;
             }
         }
+        if (G > 1u && lane < U)
+            atomicXor(&W.acc[lane % nr], sv[0]);
         if (G > 1u) {
             gw_sync();
             sv[0] = lane < nr ? W.acc[lane] : 0u;
@@ -743,6 +752,8 @@ __device__ bool gw_correct(const GwSmem &sm, GwWave &W, const RsGenParams &P, co
                 mg = alog[mod((uint32_t)lg[num] + lg[num2] + A0 - lg[den])];
             }
             W.mag[jj] = (uint8_t)mg;
+            W.lgm[jj] = mg ? (uint32_t)lg[mg] : 0xffffu;
+            W.lx[jj] = A0 - (uint32_t)W.locs[jj] - 1u;
         }
         fixed += (uint32_t)__popcll(__ballot(jj < deg && num != 0u));
     }
@@ -757,12 +768,13 @@ __device__ bool gw_correct(const GwSmem &sm, GwWave &W, const RsGenParams &P, co
             const uint32_t i = lane + 64u * q;
             if (i < nr) {
                 uint32_t acc = 0;
+                const uint32_t fi = (P.fcr + i) * P.prim;
+#pragma unroll 4
                 for (uint32_t j = 0; j < deg; ++j) {
-                    const uint32_t mj = W.mag[j];
-                    if (mj == 0u)
-                        continue;
-                    const int32_t kk = (int16_t)(uint16_t)((P.fcr + i) * P.prim * (A0 - (uint32_t)W.locs[j] - 1u));
-                    acc ^= alog[mod((uint32_t)((int32_t)lg[mj] + kk))];
+                    const uint32_t lm = W.lgm[j];
+                    const int32_t kk = (int16_t)(uint16_t)(fi * (uint32_t)W.lx[j]);
+                    const uint32_t v = alog[mod((uint32_t)((int32_t)lm + kk))];
+                    acc ^= lm == 0xffffu ? 0u : v;
                 }
                 bad |= acc != alog[W.S[i]];
             }

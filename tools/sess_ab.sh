@@ -1,6 +1,7 @@
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/tests_all.log 2>&1
-rc=$?; echo "all tests rc=$rc"; grep -E "passed|failed|Error|assert" gpurun_out/tests_all.log | tail -8
+timeout -k 10 600 python -u -m pytest tests/test_gpu_generic_wave.py -x -q --timeout 300 --timeout-method thread > gpurun_out/tests_gw.log 2>&1 && \
+timeout -k 10 400 python -u tools/general_lat.py > gpurun_out/general_lat_auto.log 2>&1
+rc=$?; echo "rc=$rc"; tail -2 gpurun_out/tests_gw.log; grep -v "^{" gpurun_out/general_lat_auto.log | cut -c1-150
 exit $rc
