@@ -1279,11 +1279,13 @@ static bool rem_release(GpuCtx &g, hipStream_t s)
  * 255-symbol ones.  Large batches of short codes keep one codeword per lane
  * (65,536 codewords of 2^m - 1 = 63 / 31 / 15: 213 / 84 / 79 us against 242
  * / 172 / 201 us per decode call; profiles/r05_general_lat_*.log) */
-static bool gen_wave(const poporon_t *h, size_t count, bool encode)
+static bool gen_wave(const poporon_t *h, size_t count, bool encode, size_t size)
 {
+    const uint32_t nn = h->rs->gf->field_size;
+    if (size < 1 || size + h->rs->num_roots > nn) /* the wave kernels hold one row of <= nn symbols */
+        return false;
     if (h->gen_path)
         return h->gen_path == 2;
-    const uint32_t nn = h->rs->gf->field_size;
     return count < 16384 || (encode ? nn == 255u : nn >= 127u);
 }
 
@@ -1305,8 +1307,8 @@ static bool launch_encode(poporon_t *h, const uint8_t *d_data, size_t ds, uint8_
     } else {
         RsGenParams prm = h->gen;
         prm.size = (uint32_t)size;
-        if (gen_wave(h, count, true))
-            HIP_OK(rsgw_encode(h->gpu.gtab, &prm, d_data, ds, d_par, ps, count, h->gpu.num_cu, s));
+        if (gen_wave(h, count, true, size))
+            HIP_OK(rsgw_encode(h->gpu.gtab, &prm, d_data, ds, d_par, ps, count, nullptr, 0u, h->gpu.num_cu, s));
         else
             HIP_OK(rsg_encode(h->gpu.gtab, &prm, d_data, ds, d_par, ps, count, h->gpu.num_cu, s));
     }
@@ -1379,7 +1381,7 @@ static bool launch_split(poporon_t *h, const RsCorrParams &prm, const RsSplitWs 
                                        nullptr, 0, nullptr, ok, corrected, g.num_cu, s));
             else
                 HIP_OK(rsgw_decode(g.gtab, &gp, d_data, ds, d_par, ps, count, ext, ext_stride, nullptr, nullptr, 0,
-                                   nullptr, ok, corrected, ws.list, ws.nlist, g.num_cu, s));
+                                   nullptr, ok, corrected, ws.list, ws.nlist, nullptr, 0u, g.num_cu, s));
         } else {
             HIP_OK(rsk_wave(g.tab, &prm, d_data, ds, d_par, ps, count, ws.list, ws.nlist, ext ? nullptr : ws.syn, ext,
                             ext_stride, nullptr, nullptr, 0, nullptr, ok, corrected, g.num_cu, s));
@@ -1491,7 +1493,7 @@ static bool launch_decode(poporon_t *h, uint8_t *d_data, size_t ds, uint8_t *d_p
                                        pos_stride, cnt, ok, corrected, g.num_cu, s));
             else
                 HIP_OK(rsgw_decode(g.gtab, &gp, d_data, ds, d_par, ps, count, nullptr, 0, pos8, nullptr, pos_stride,
-                                   cnt, ok, corrected, ws.list, ws.nlist, g.num_cu, s));
+                                   cnt, ok, corrected, ws.list, ws.nlist, nullptr, 0u, g.num_cu, s));
             t.done();
         }
         {
@@ -1506,9 +1508,9 @@ static bool launch_decode(poporon_t *h, uint8_t *d_data, size_t ds, uint8_t *d_p
         prm.size = (uint32_t)size;
         prm.pad = (int32_t)(h->rs->gf->field_size - h->rs->num_roots - size);
         KernelTimer t(h->gpu, POPORON_AMD_KERNEL_CORRECT, s);
-        if (gen_wave(h, count, false))
+        if (gen_wave(h, count, false, size))
             HIP_OK(rsgw_decode(h->gpu.gtab, &prm, d_data, ds, d_par, ps, count, ext_syn, ext_stride, pos8, pos32,
-                               pos_stride, cnt, ok, corrected, nullptr, nullptr, h->gpu.num_cu, s));
+                               pos_stride, cnt, ok, corrected, nullptr, nullptr, nullptr, 0u, h->gpu.num_cu, s));
         else
             HIP_OK(rsg_decode(h->gpu.gtab, &prm, d_data, ds, d_par, ps, count, ext_syn, ext_stride, pos8, pos32,
                               pos_stride, cnt, ok, corrected, h->gpu.num_cu, s));
@@ -1682,8 +1684,12 @@ EXPORT bool poporon_check_batch_device(poporon_t *h, const uint8_t *d_data, size
     } else {
         RsGenParams prm = h->gen;
         prm.size = (uint32_t)size;
-        HIP_OK(rsg_check(h->gpu.gtab, &prm, d_data, data_stride, d_parity, parity_stride, count, d_dirty, nullptr,
-                         0, h->gpu.num_cu, s));
+        if (gen_wave(h, count, false, size))
+            HIP_OK(rsgw_check(h->gpu.gtab, &prm, d_data, data_stride, d_parity, parity_stride, count, d_dirty,
+                              nullptr, 0, h->gpu.num_cu, s));
+        else
+            HIP_OK(rsg_check(h->gpu.gtab, &prm, d_data, data_stride, d_parity, parity_stride, count, d_dirty,
+                             nullptr, 0, h->gpu.num_cu, s));
     }
     t.done();
     return true;
@@ -1723,8 +1729,12 @@ EXPORT bool poporon_syndrome_batch_device(poporon_t *h, const uint8_t *d_data, s
         RsGenParams prm = h->gen;
         prm.size = (uint32_t)size;
         KernelTimer t(h->gpu, POPORON_AMD_KERNEL_REMAINDER, s);
-        HIP_OK(rsg_check(h->gpu.gtab, &prm, d_data, data_stride, d_parity, parity_stride, count, d_nonzero,
-                         d_syndromes, syndrome_stride, h->gpu.num_cu, s));
+        if (gen_wave(h, count, false, size))
+            HIP_OK(rsgw_check(h->gpu.gtab, &prm, d_data, data_stride, d_parity, parity_stride, count, d_nonzero,
+                              d_syndromes, syndrome_stride, h->gpu.num_cu, s));
+        else
+            HIP_OK(rsg_check(h->gpu.gtab, &prm, d_data, data_stride, d_parity, parity_stride, count, d_nonzero,
+                             d_syndromes, syndrome_stride, h->gpu.num_cu, s));
         t.done();
         return true;
     }
@@ -2381,6 +2391,21 @@ EXPORT bool poporon_encode(poporon_t *h, uint8_t *data, size_t size, uint8_t *pa
         memcpy(parity, g.zc + ZC_PAR, nr);
         return true;
     }
+    /* general parameters: rsgw_encode_k on coherent host memory, the same way */
+    if (h->fec_type == PPLN_FEC_RS && h->generic && gen_wave(h, 1, true, size) && ensure_zc(g)) {
+        memcpy(g.zc + GZ_DATA, data, size);
+        RsGenParams prm = h->gen;
+        prm.size = (uint32_t)size;
+        const uint32_t seq = ++g.zc_seq;
+        KernelTimer t(g, POPORON_AMD_KERNEL_ENCODE, g.stream);
+        HIP_OK(rsgw_encode(g.gtab, &prm, g.zc_dev + GZ_DATA, size, g.zc_dev + GZ_PAR, nr, 1,
+                           reinterpret_cast<uint32_t *>(g.zc_dev + ZC_FLAG), seq, g.num_cu, g.stream));
+        t.done();
+        if (!zc_wait(g, seq))
+            return false;
+        memcpy(parity, g.zc + GZ_PAR, nr);
+        return true;
+    }
     const size_t off_p = (size + 15) & ~(size_t)15;
     if (!ensure_stage(h, off_p + nr + 16))
         return false;
@@ -2489,6 +2514,53 @@ static bool rs_decode_one(poporon_t *h, uint8_t *data, size_t size, uint8_t *par
             memcpy(parity, z + ZC_PAR, nr);
             success = z[ZC_OK] != 0;
             fixed = z[ZC_COR];
+        } else if (gen_wave(h, 1, false, size) && ensure_zc(g)) {
+            /* general parameters, one wave (rsgw_decode_k): the row, the slots
+             * or the external syndromes read from coherent host memory, the
+             * corrected bytes, ok and corrected_num written back there, then
+             * the completion word (no copies, no stream synchronisation) */
+            const uint32_t nn = h->rs->gf->field_size;
+            uint8_t *z = g.zc, *zd = g.zc_dev;
+            memcpy(z + GZ_DATA, data, size);
+            memcpy(z + GZ_PAR, parity, nr);
+            const uint16_t *ext = nullptr;
+            const uint32_t *pos32 = nullptr;
+            const uint8_t *cnt = nullptr;
+            bool refuse = false;
+            if (h->ext_syndrome) {
+                for (size_t i = 0; i < nr; i++)
+                    refuse |= h->ext_syndrome[i] > nn; /* out-of-table index in the reference */
+                memcpy(z + GZ_EXT, h->ext_syndrome, nr * sizeof(uint16_t));
+                ext = reinterpret_cast<const uint16_t *>(zd + GZ_EXT);
+            } else if (h->erasure) {
+                const poporon_erasure_t *e = h->erasure;
+                uint32_t *pos = reinterpret_cast<uint32_t *>(z + GZ_POS);
+                const size_t have = std::min<size_t>(e->capacity, nr); /* stale slots read as the reference (Q2/Q3) */
+                memcpy(pos, e->erasure_positions, have * sizeof(uint32_t));
+                memset(pos + have, 0, (nr - have) * sizeof(uint32_t));
+                z[GZ_CNT] = (uint8_t)std::min<uint32_t>(e->erasure_count, 255u); /* past nr: refused if dirty (Q5) */
+                pos32 = reinterpret_cast<const uint32_t *>(zd + GZ_POS);
+                cnt = zd + GZ_CNT;
+            }
+            if (refuse) {
+                fail("external syndrome > field size: undefined in the reference, refused");
+            } else {
+                RsGenParams prm = h->gen;
+                prm.size = (uint32_t)size;
+                prm.pad = (int32_t)(nn - nr - size);
+                const uint32_t seq = ++g.zc_seq;
+                KernelTimer t(g, POPORON_AMD_KERNEL_CORRECT, g.stream);
+                HIP_OK(rsgw_decode(g.gtab, &prm, zd + GZ_DATA, size, zd + GZ_PAR, nr, 1, ext, nr, nullptr, pos32, nr,
+                                   cnt, zd + GZ_OK, zd + GZ_COR, nullptr, nullptr,
+                                   reinterpret_cast<uint32_t *>(zd + ZC_FLAG), seq, g.num_cu, g.stream));
+                t.done();
+                if (!zc_wait(g, seq))
+                    return false;
+                memcpy(data, z + GZ_DATA, size);
+                memcpy(parity, z + GZ_PAR, nr);
+                success = z[GZ_OK] != 0;
+                fixed = z[GZ_COR];
+            }
         } else {
             /* general parameters (rs_generic.hip): everything through the pinned
              * mirror, one H2D copy of [data | parity | ok | cor | pad | syndromes

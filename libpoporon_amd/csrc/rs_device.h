@@ -213,7 +213,16 @@ hipError_t rsk_serve(const RsDevTables *tab, const RsCorrParams *prm, uint8_t *z
 #define ZC_REQ_MODE(w) (((w) >> 10) & 3u) /* decode mode (rsk_decode1) */
 #define ZC_REQ_SIZE(w) ((w) & 0xFFu)      /* message bytes (1..223) */
 #define ZC_EXITED 768 /* u32: the id of the last server launch that has left */
-#define ZC_BYTES 1024
+/* general-parameter single calls (rsgw_*_k, one wave): a row of up to 255
+ * symbols, up to 254 u32 slots / u16 syndromes */
+#define GZ_DATA 1024 /* message / data bytes */
+#define GZ_PAR 1280  /* parity bytes */
+#define GZ_POS 1536  /* erasure slots, u32 */
+#define GZ_CNT 2560  /* erasure count, u8 */
+#define GZ_EXT 2576  /* external syndromes, u16 */
+#define GZ_OK 3088
+#define GZ_COR 3089
+#define ZC_BYTES 4096
 #define RS_SRV_ENCODE 1u
 #define RS_SRV_DECODE 2u
 #define RS_SRV_STOP 3u   /* the server leaves (poporon_destroy) */

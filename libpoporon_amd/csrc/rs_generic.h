@@ -35,12 +35,20 @@ extern "C" {
 /* one codeword per wave (latency: single calls, small batches, lists,
  * long root counts); same arguments and results as rsg_encode / rsg_decode,
  * list / list_n as rsg_decode_list */
+/* flag / seq (single calls on coherent host memory): the kernel stores seq
+ * to *flag with a system-scope release after every result */
 hipError_t rsgw_encode(const RsGenTables *tab, const RsGenParams *prm, const uint8_t *data, size_t dstride,
-                       uint8_t *parity, size_t pstride, size_t count, int num_cu, hipStream_t stream);
+                       uint8_t *parity, size_t pstride, size_t count, uint32_t *flag, uint32_t seq, int num_cu,
+                       hipStream_t stream);
 hipError_t rsgw_decode(const RsGenTables *tab, const RsGenParams *prm, uint8_t *data, size_t dstride, uint8_t *parity,
                        size_t pstride, size_t count, const uint16_t *ext, size_t ext_stride, const uint8_t *pos8,
                        const uint32_t *pos32, size_t pos_stride, const uint8_t *cnt, uint8_t *ok, uint8_t *corrected,
-                       const uint32_t *list, const uint32_t *list_n, int num_cu, hipStream_t stream);
+                       const uint32_t *list, const uint32_t *list_n, uint32_t *flag, uint32_t seq, int num_cu,
+                       hipStream_t stream);
+
+hipError_t rsgw_check(const RsGenTables *tab, const RsGenParams *prm, const uint8_t *data, size_t dstride,
+                      const uint8_t *parity, size_t pstride, size_t count, uint8_t *dirty, uint16_t *syn,
+                      size_t syn_stride, int num_cu, hipStream_t stream);
 
 hipError_t rsg_encode(const RsGenTables *tab, const RsGenParams *prm, const uint8_t *data, size_t dstride,
                       uint8_t *parity, size_t pstride, size_t count, int num_cu, hipStream_t stream);

@@ -427,6 +427,7 @@ __global__ __launch_bounds__(G_WG_MAX) void rsg_check_k(const RsGenTables *__res
 #define GW_WG 256
 #define GW_Z 512u   /* log of zero in the sentinel arrays: any sum with it indexes al2's zero part */
 #define GW_AL2 1536 /* al2[x] = alpha^(x mod nn) for x < 2 nn, 0 from there on */
+#define GW_QS 16384 /* max size * nr with size + nr <= 255: 127 * 128 (u16: 32 KB) */
 
 struct GwWave {
     uint8_t cw[256];    /* the received row [data | parity], raw bytes */
@@ -454,6 +455,18 @@ __device__ __forceinline__ void gw_sync()
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+/* single calls on coherent host memory: every store of the block
+ * acknowledged, then one system-scope release of the completion word */
+__device__ __forceinline__ void gw_done(uint32_t *flag, uint32_t seq)
+{
+    if (flag) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (threadIdx.x == 0)
+            __hip_atomic_store(flag, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
 }
 
 /* XOR over the wave, in every lane (permlane swaps across halves and rows,
@@ -485,13 +498,22 @@ __device__ __forceinline__ void gw_shift(const uint32_t (&v)[4], uint32_t (&out)
     }
 }
 
+/* the tables: one global load per thread and table, al2 from the LDS copy
+ * (its six entries per thread loaded from global one after another had cost
+ * a few us per launch) */
+__device__ __forceinline__ void gw_fill_al2(uint8_t *al2, const uint8_t *alog_lds, uint32_t nn)
+{
+    for (uint32_t x = threadIdx.x; x < GW_AL2; x += GW_WG)
+        al2[x] = x < nn ? alog_lds[x] : (x < 2u * nn ? alog_lds[x - nn] : (uint8_t)0);
+}
+
 __device__ __forceinline__ void gw_tables(GwSmem &sm, const RsGenTables *__restrict__ T, uint32_t nn)
 {
     const uint32_t t = threadIdx.x;
     sm.alog[t] = T->alog[t];
     sm.log[t] = T->log[t];
-    for (uint32_t x = t; x < GW_AL2; x += GW_WG)
-        sm.al2[x] = x < nn ? T->alog[x] : (x < 2u * nn ? T->alog[x - nn] : (uint8_t)0);
+    __syncthreads();
+    gw_fill_al2(sm.al2, sm.alog, nn);
 }
 
 /* syndromes of the row in W.cw / W.lr into W.S / W.sz; true if any is nonzero
@@ -683,6 +705,7 @@ __device__ bool gw_correct(const GwSmem &sm, GwWave &W, const RsGenParams &P, co
             acc[q] = 1;
             tt[q] = 0;
         }
+#pragma unroll 4
         for (uint32_t j = 1; j <= deg; ++j) {
             const uint32_t lz = W.lamz[j];
 #pragma unroll
@@ -720,6 +743,7 @@ __device__ bool gw_correct(const GwSmem &sm, GwWave &W, const RsGenParams &P, co
         const uint32_t i = lane + 64u * q;
         if (i < deg) {
             uint32_t acc = 0;
+#pragma unroll 4
             for (uint32_t j = 0; j <= i; ++j)
                 acc ^= al2[W.sz[i - j] + W.lamz[j]];
             W.omz[i] = acc ? lg[acc] : GW_Z;
@@ -738,6 +762,7 @@ __device__ bool gw_correct(const GwSmem &sm, GwWave &W, const RsGenParams &P, co
             const uint32_t rt = W.roots[jj];
             const uint32_t rm = rt >= nn ? rt - nn : rt;
             uint32_t t = 0;
+#pragma unroll 4
             for (uint32_t i = 0; i < deg; ++i) {
                 num ^= al2[W.omz[i] + t];
                 t += rm;
@@ -747,6 +772,7 @@ __device__ bool gw_correct(const GwSmem &sm, GwWave &W, const RsGenParams &P, co
             if (num != 0u) {
                 const uint32_t num2 = alog[mod((uint32_t)((int32_t)rt * ((int32_t)P.fcr - 1) + (int32_t)A0))];
                 uint32_t den = 0;
+#pragma unroll 4
                 for (int32_t i = (int32_t)dtop; i >= 0; i -= 2)
                     den ^= al2[W.lamz[(uint32_t)i + 1u] + mod((uint32_t)i * rt)];
                 mg = alog[mod((uint32_t)lg[num] + lg[num2] + A0 - lg[den])];
@@ -855,7 +881,8 @@ __global__ __launch_bounds__(GW_WG) void rsgw_decode_k(const RsGenTables *__rest
                                                         const uint8_t *__restrict__ cntv, uint8_t *__restrict__ ok,
                                                         uint8_t *__restrict__ corrected,
                                                         const uint32_t *__restrict__ list,
-                                                        const uint32_t *__restrict__ list_n)
+                                                        const uint32_t *__restrict__ list_n, uint32_t *flag,
+                                                        uint32_t seq)
 {
     const size_t n = list ? (size_t)*list_n : count;
     if ((size_t)blockIdx.x * (GW_WG / 64) >= n)
@@ -920,6 +947,49 @@ __global__ __launch_bounds__(GW_WG) void rsgw_decode_k(const RsGenTables *__rest
         }
         gw_sync();
     }
+    gw_done(flag, seq);
+}
+
+/* check / syndromes, one codeword per wave (rsg_check_k's outputs) */
+__global__ __launch_bounds__(GW_WG) void rsgw_check_k(const RsGenTables *__restrict__ T, RsGenParams P,
+                                                       const uint8_t *__restrict__ data, size_t dstride,
+                                                       const uint8_t *__restrict__ parity, size_t pstride,
+                                                       size_t count, uint8_t *__restrict__ dirty,
+                                                       uint16_t *__restrict__ syn, size_t syn_stride)
+{
+    if ((size_t)blockIdx.x * (GW_WG / 64) >= count)
+        return;
+    __shared__ GwSmem sm;
+    const uint32_t t = threadIdx.x, lane = t & 63u, wave = t >> 6;
+    gw_tables(sm, T, P.nn);
+    __syncthreads();
+    GwWave &W = sm.w[wave];
+    const GMod mod{P.nn, P.magic};
+    const uint32_t nr = P.nroots, A0 = P.nn, size = P.size, total = size + nr;
+    const bool qf = (P.fcr + nr - 1u) * P.prim + A0 - 1u < 65536u;
+    for (size_t e = (size_t)blockIdx.x * (GW_WG / 64) + wave; e < count; e += (size_t)gridDim.x * (GW_WG / 64)) {
+        const uint8_t *d = data + e * dstride, *par = parity + e * pstride;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const uint32_t b = lane + 64u * q;
+            const uint32_t v = b < size ? d[b] : (b < total ? par[b - size] : 0u);
+            const uint32_t m = v & A0;
+            W.cw[b] = (uint8_t)v;
+            W.lr[b] = m ? (uint32_t)sm.log[m] : GW_Z;
+        }
+        gw_sync();
+        const bool nz = gw_syndromes(sm, W, P, mod, lane, qf);
+        if (dirty && lane == 0u)
+            dirty[e] = nz ? 1 : 0;
+        if (syn) /* log form, the reference's uint16 array (src/decode.c:409-412) */
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const uint32_t i = lane + 64u * q;
+                if (i < nr)
+                    syn[e * syn_stride + i] = W.S[i];
+            }
+        gw_sync();
+    }
 }
 
 /* Encode, one message per wave: parity = sum_b d_b Q[size - 1 - b], Q[d] the
@@ -928,18 +998,56 @@ __global__ __launch_bounds__(GW_WG) void rsgw_decode_k(const RsGenTables *__rest
  * in the masked message bytes); lane p (and p + 64 ...) owns parity byte p */
 __global__ __launch_bounds__(GW_WG) void rsgw_encode_k(const RsGenTables *__restrict__ T, RsGenParams P,
                                                         const uint8_t *__restrict__ data, size_t dstride,
-                                                        uint8_t *__restrict__ parity, size_t pstride, size_t count)
+                                                        uint8_t *__restrict__ parity, size_t pstride, size_t count,
+                                                        uint32_t *flag, uint32_t seq)
 {
+    /* single calls and tiny batches of messages longer than their parity:
+     * lanes over the message bytes (nr reductions) rather than over the
+     * parity bytes (size serial steps): RS(255,207) 25 vs 43 us per call,
+     * RS(255,55) 46 vs 31 (profiles/r05_general_lat_auto.log) */
+    const bool by_byte = count <= 64u && P.size > P.nroots;
     if ((size_t)blockIdx.x * (GW_WG / 64) >= count)
         return;
     __shared__ uint8_t al2[GW_AL2];
     __shared__ uint8_t lg[256];
     __shared__ uint16_t lr[GW_WG / 64][256];
+    __shared__ uint16_t qs[GW_QS]; /* the rows Q[0 .. size) packed (nr logs each, GW_Z: zero): size + nr <= 255 */
+    __shared__ uint8_t alog[256];
     const uint32_t t = threadIdx.x, lane = t & 63u, wave = t >> 6;
     const uint32_t nn = P.nn, A0 = P.nn, nr = P.nroots, size = P.size;
     lg[t] = T->log[t];
-    for (uint32_t x = t; x < GW_AL2; x += GW_WG)
-        al2[x] = x < nn ? T->alog[x] : (x < 2u * nn ? T->alog[x - nn] : (uint8_t)0);
+    alog[t] = T->alog[t];
+    /* 16-byte chunks of the rows, up to four per thread issued before any is
+     * used (a row per step, one load at a time, had cost ~0.3 us each) */
+    {
+        const uint32_t cpr = (nr + 15u) / 16u, nch = size * cpr;
+        for (uint32_t x0 = t; x0 < nch; x0 += 4u * GW_WG) {
+            uint4 v[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const uint32_t x = x0 + (uint32_t)k * GW_WG;
+                if (x < nch)
+                    v[k] = *reinterpret_cast<const uint4 *>(T->encq + (x / cpr) * 256u + (x % cpr) * 16u);
+            }
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const uint32_t x = x0 + (uint32_t)k * GW_WG;
+                if (x < nch) {
+                    const uint32_t r = x / cpr, c = x % cpr;
+                    const uint32_t w[4] = {v[k].x, v[k].y, v[k].z, v[k].w};
+#pragma unroll
+                    for (int j = 0; j < 16; ++j) {
+                        const uint32_t pp = c * 16u + (uint32_t)j;
+                        const uint32_t b = (w[j >> 2] >> (8 * (j & 3))) & 0xffu;
+                        if (pp < nr)
+                            qs[r * nr + pp] = b == 0xffu ? GW_Z : b;
+                    }
+                }
+            }
+        }
+    }
+    __syncthreads();
+    gw_fill_al2(al2, alog, nn);
     __syncthreads();
     for (size_t e = (size_t)blockIdx.x * (GW_WG / 64) + wave; e < count; e += (size_t)gridDim.x * (GW_WG / 64)) {
         const uint8_t *d = data + e * dstride;
@@ -953,18 +1061,36 @@ __global__ __launch_bounds__(GW_WG) void rsgw_encode_k(const RsGenTables *__rest
         }
         gw_sync();
         uint32_t acc[4] = {0, 0, 0, 0};
+        const uint32_t nq = (nr + 63u) / 64u;
+        if (by_byte) {
+            /* lanes over the message bytes (b = lane + 64 k), one XOR reduction
+             * per parity byte: nr short steps instead of size serial ones */
+            uint32_t lb[4], rb[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const uint32_t b = lane + 64u * k;
+                lb[k] = b < size ? (uint32_t)lr[wave][b] : GW_Z;
+                rb[k] = b < size ? (size - 1u - b) * nr : 0u;
+            }
+            for (uint32_t p = 0; p < nr; ++p) {
+                uint32_t x = 0;
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+                    x ^= al2[lb[k] + qs[rb[k] + p]];
+                x = gw_xor(x);
+                if ((p & 63u) == lane)
+                    acc[p >> 6] = x;
+            }
+        } else
+#pragma unroll 4
         for (uint32_t b = 0; b < size; ++b) {
-            const uint32_t l = lr[wave][b];
-            if (l == GW_Z)
-                continue;
-            const uint8_t *row = T->encq + (size_t)(size - 1u - b) * 256u;
+            const uint32_t l = lr[wave][b]; /* zero byte or zero entry: a sentinel sum, al2's zero part */
+            const uint16_t *row = qs + (size - 1u - b) * nr;
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
                 const uint32_t p = lane + 64u * q;
-                if (p < nr) {
-                    const uint32_t qe = row[p];
-                    acc[q] ^= qe == 0xffu ? 0u : (uint32_t)al2[l + qe];
-                }
+                if ((uint32_t)q < nq && p < nr)
+                    acc[q] ^= al2[l + row[p]];
             }
         }
         uint8_t *out = parity + e * pstride;
@@ -976,6 +1102,7 @@ __global__ __launch_bounds__(GW_WG) void rsgw_encode_k(const RsGenTables *__rest
         }
         gw_sync();
     }
+    gw_done(flag, seq);
 }
 
 /* ------------------------------------------------------------------------ */
@@ -1077,12 +1204,13 @@ static dim3 gw_grid(size_t waves, int num_cu)
 }
 
 extern "C" hipError_t rsgw_encode(const RsGenTables *tab, const RsGenParams *prm, const uint8_t *data, size_t dstride,
-                                  uint8_t *parity, size_t pstride, size_t count, int num_cu, hipStream_t stream)
+                                  uint8_t *parity, size_t pstride, size_t count, uint32_t *flag, uint32_t seq,
+                                  int num_cu, hipStream_t stream)
 {
     if (count == 0)
         return hipSuccess;
     RS_LAUNCH(rsgw_encode_k, gw_grid(count, num_cu), dim3(GW_WG), 0, stream, tab, *prm, data, dstride, parity, pstride,
-              count);
+              count, flag, seq);
     return hipGetLastError();
 }
 
@@ -1090,7 +1218,7 @@ extern "C" hipError_t rsgw_decode(const RsGenTables *tab, const RsGenParams *prm
                                   uint8_t *parity, size_t pstride, size_t count, const uint16_t *ext, size_t ext_stride,
                                   const uint8_t *pos8, const uint32_t *pos32, size_t pos_stride, const uint8_t *cnt,
                                   uint8_t *ok, uint8_t *corrected, const uint32_t *list, const uint32_t *list_n,
-                                  int num_cu, hipStream_t stream)
+                                  uint32_t *flag, uint32_t seq, int num_cu, hipStream_t stream)
 {
     if (count == 0)
         return hipSuccess;
@@ -1098,9 +1226,20 @@ extern "C" hipError_t rsgw_decode(const RsGenTables *tab, const RsGenParams *prm
     const dim3 grid = gw_grid(list ? (count + 15) / 16 : count, num_cu);
     if (pos32)
         RS_LAUNCH(rsgw_decode_k<uint32_t>, grid, dim3(GW_WG), 0, stream, tab, *prm, data, dstride, parity, pstride,
-                  count, ext, ext_stride, pos32, pos_stride, cnt, ok, corrected, list, list_n);
+                  count, ext, ext_stride, pos32, pos_stride, cnt, ok, corrected, list, list_n, flag, seq);
     else
         RS_LAUNCH(rsgw_decode_k<uint8_t>, grid, dim3(GW_WG), 0, stream, tab, *prm, data, dstride, parity, pstride,
-                  count, ext, ext_stride, pos8, pos_stride, cnt, ok, corrected, list, list_n);
+                  count, ext, ext_stride, pos8, pos_stride, cnt, ok, corrected, list, list_n, flag, seq);
+    return hipGetLastError();
+}
+
+extern "C" hipError_t rsgw_check(const RsGenTables *tab, const RsGenParams *prm, const uint8_t *data, size_t dstride,
+                                 const uint8_t *parity, size_t pstride, size_t count, uint8_t *dirty, uint16_t *syn,
+                                 size_t syn_stride, int num_cu, hipStream_t stream)
+{
+    if (count == 0)
+        return hipSuccess;
+    RS_LAUNCH(rsgw_check_k, gw_grid(count, num_cu), dim3(GW_WG), 0, stream, tab, *prm, data, dstride, parity, pstride,
+              count, dirty, syn, syn_stride);
     return hipGetLastError();
 }

@@ -144,3 +144,40 @@ def test_generic_external_syndromes_vs_oracle(torch_cuda, params, path, monkeypa
         assert gok[c] == wok and gcor[c] == wn, (c, c % 4)
         assert (got[c, :k] == wd).all() and (got[c, k:] == wp).all(), (c, c % 4)
     h.close()
+
+
+@pytest.mark.parametrize("path", ["wave", "lane"])
+@pytest.mark.parametrize("params", _PARAMS)
+def test_generic_check_and_syndromes_vs_oracle(torch_cuda, params, path, monkeypatch):
+    """poporon_check_batch_device / poporon_syndrome_batch_device on the
+    general kernels (rsgw_check_k / rsg_check_k; the fewer-roots sets on the
+    LFSR kernel): dirty flags and log-form syndromes equal the oracle's."""
+    from oracle import Oracle
+    torch = torch_cuda
+    monkeypatch.setenv("POPORON_AMD_GENERIC", path)
+    m, poly, fcr, prim, nr = params
+    o, h = Oracle(*params), P.Poporon(*params)
+    nn = (1 << m) - 1
+    rng = np.random.default_rng(nr * 5 + m)
+    s = torch.cuda.current_stream().cuda_stream
+    n = 200
+    for size in sorted({nn - nr, max(1, (nn - nr) // 3)}):
+        data, par = _rows(rng, o, n, size, nn)
+        cw = np.concatenate([data, par], 1)
+        for c in range(n):
+            ne = c % 3
+            cw[c, rng.permutation(size + nr)[:ne]] ^= rng.integers(1, nn + 1, ne).astype(np.uint8)
+        dev = torch.from_numpy(cw).cuda()
+        b, w = dev.data_ptr(), size + nr
+        dirty = torch.full((n,), 7, dtype=torch.uint8, device="cuda")
+        h.check_batch_device(b, w, b + size, w, size, n, dirty.data_ptr(), s)
+        syn = torch.zeros((n, nr), dtype=torch.int16, device="cuda")
+        nz = torch.full((n,), 7, dtype=torch.uint8, device="cuda")
+        h.syndrome_batch_device(b, w, b + size, w, size, n, syn.data_ptr(), nr, nz.data_ptr(), s)
+        torch.cuda.synchronize()
+        got = syn.cpu().numpy().astype(np.uint16)
+        gd, gn = dirty.cpu().numpy(), nz.cpu().numpy()
+        for c in range(n):
+            f, want = o.syndrome(cw[c, :size], cw[c, size:])
+            assert bool(gd[c]) == f and bool(gn[c]) == f and (got[c] == want).all(), (size, c)
+    h.close()
