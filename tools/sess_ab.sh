@@ -1,7 +1,6 @@
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-timeout -k 10 600 python -u -m pytest tests/test_gpu_generic_wave.py tests/test_gpu_parity.py tests/test_gpu_single.py -x -q --timeout 300 --timeout-method thread > gpurun_out/tests_gw.log 2>&1 && \
-timeout -k 10 400 python -u tools/general_lat.py > gpurun_out/general_lat_auto.log 2>&1
-rc=$?; echo "rc=$rc"; tail -3 gpurun_out/tests_gw.log; grep -v "^{" gpurun_out/general_lat_auto.log | cut -c1-100
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/tests_all.log 2>&1
+rc=$?; echo "all tests rc=$rc"; grep -E "passed|failed|Error|assert" gpurun_out/tests_all.log | tail -8
 exit $rc
