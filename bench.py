@@ -931,7 +931,7 @@ def general_params(be, n=1 << 20, reps=5, params=(8, 0x11D, 1, 1, 16), nerr=8):
     for kid, name in P.KERNEL_NAMES.items():
         ms, cnt = h.timing_read(kid)
         if cnt:  # (the hand-off list of a code with < 32 roots runs on the general kernel)
-            kms[name.replace("rs_wave_k (list)", "rsg_decode_k (list)")] = round(ms / cnt, 4)
+            kms[name.replace("rs_wave_k (list)", "rsgw_decode_k (list)")] = round(ms / cnt, 4)
     h.timing(False)
     nbad += be.n_bad((ok, cor), nerr) + be.n_diff(rows, clean)
     idx = sample_index(n)
@@ -969,7 +969,7 @@ def general_params(be, n=1 << 20, reps=5, params=(8, 0x11D, 1, 1, 16), nerr=8):
     return {"code": f"RS(255,{k}): symbol_size {m}, poly {poly:#x}, fcr {fcr}, prim {prim}, {nr} roots",
             "kernels": "encode: rs_lfsr_k<ENCODE> with g(x) x^(32 - nr) (rsk_encode_nr); decode: the split "
                        "kernels with npar = nr (rsk_syndrome_reset_nr, rs_bm_k<true>, rs_chien_k, rs_forney_k, "
-                       "rsk_apply_nr; hand-off list on rsg_decode_k); erasure decode: the errata kernels with npar "
+                       "rsk_apply_nr; hand-off list on rsgw_decode_k); erasure decode: the errata kernels with npar "
                        "= nr (rsk_ebm_nr, rs_chien32_k, rsk_forney32_nr, rsk_apply_era_nr)", "codewords": n,
             "errors_per_codeword": nerr,
             "encode_cw_per_s": round(n / e, 1), "decode_cw_per_s": round(n / d, 1),
