@@ -983,6 +983,80 @@ def general_params(be, n=1 << 20, reps=5, params=(8, 0x11D, 1, 1, 16), nerr=8):
             "sample": {"checker": "port: oracle/rs_oracle.c (pinned)", "n": int(len(idx)), "mismatches": mism}}
 
 
+def general_wave(be, sets=((8, 0x11D, 1, 1, 100), (4, 0x13, 1, 2, 8)), n=1 << 16, calls=200, reps=3):
+    """SURVEY 8(f) row 1 beyond the fewer-roots codes: parameter sets of the
+    reference's own tests that run on the general kernels (rs_generic.hip) --
+    RS(255,155) (100 roots: one codeword per wave, rsgw_*) and RS(15,7) over
+    GF(16) with prim 2 (single calls on rsgw_*, its large batches one
+    codeword per lane, rsg_*): single-call encode / decode latency through
+    ctypes (t errors) and a device batch of n codewords with t errors each
+    (wall, stream-synchronised, median of reps).  Every 256th batch codeword
+    and every single call are compared with the oracle restatement."""
+    import numpy as np
+
+    from oracle import Oracle
+    torch, P = be.torch, be.P
+    s = be.stream
+    out = {}
+    for params in sets:
+        m, poly, fcr, prim, nr = params
+        nn = (1 << m) - 1
+        k, t = nn - nr, nr // 2
+        h, o = P.Poporon(*params, device=be.local), Oracle(*params)
+        rng = np.random.default_rng(SEED + nr + m)
+        data = rng.integers(0, nn + 1, (n, k), dtype=np.uint8)
+        par = h.encode_batch(data)
+        mism = int((par[::256] != o.encode_batch(data[::256])).any(1).sum())
+        cw = np.concatenate([data, par], 1)
+        pos = np.argsort(rng.random((n, nn)), axis=1)[:, :t]
+        bad = cw.copy()
+        np.bitwise_xor.at(bad, (np.arange(n)[:, None], pos), rng.integers(1, nn + 1, (n, t), dtype=np.uint8))
+        # single calls
+        h.encode(data[0])
+        t0 = time.perf_counter()
+        spar = [h.encode(data[i]) for i in range(calls)]
+        te = (time.perf_counter() - t0) / calls
+        mism += sum(int((spar[i] != par[i]).any()) for i in range(calls))
+        h.decode(bad[0, :k], bad[0, k:])
+        t0 = time.perf_counter()
+        res = [h.decode(bad[i, :k], bad[i, k:]) for i in range(calls)]
+        td = (time.perf_counter() - t0) / calls
+        for i in range(calls):
+            wok, wn, wd, wp = o.decode(bad[i, :k], bad[i, k:])
+            mism += int(res[i][0] != wok or res[i][1] != wn or (res[i][2] != wd).any() or (res[i][3] != wp).any())
+        # device batch
+        src = torch.from_numpy(bad).to(be.dev)
+        buf = src.clone()
+        ok, cor = be.status(n)
+        b = buf.data_ptr()
+        tb = []
+        for r in range(reps + 1):
+            buf.copy_(src)
+            be.sync()
+            t0 = time.perf_counter()
+            h.decode_batch_device(b, nn, b + k, nn, k, n, ok.data_ptr(), cor.data_ptr(), stream=s)
+            be.sync()
+            if r:
+                tb.append(time.perf_counter() - t0)
+        got, gok, gcor = buf.cpu().numpy(), ok.cpu().numpy(), cor.cpu().numpy()
+        idx = np.arange(0, n, 256)
+        ook, ocor, od, op = o.decode_batch(bad[idx, :k], bad[idx, k:])
+        mism += int(((ook != gok[idx]) | (ocor != gcor[idx]) | (od != got[idx, :k]).any(1) |
+                     (op != got[idx, k:]).any(1)).sum())
+        mism += int((got != cw).any(1).sum())  # t errors: every codeword back to the encoded row
+        d = float(np.median(tb))
+        out[f"RS({nn},{k})"] = {
+            "params": {"symbol_size": m, "poly": hex(poly), "fcr": fcr, "prim": prim, "num_roots": nr},
+            "single_encode_us": round(te * 1e6, 1), "single_decode_us": round(td * 1e6, 1),
+            "batch_codewords": n, "batch_decode_cw_per_s": round(n / d, 1), "batch_decode_ms": round(d * 1e3, 4),
+            "errors_per_codeword": t, "mismatches": mism}
+        h.close()
+    out["note"] = ("single calls: poporon_encode / poporon_decode through ctypes (one wave, coherent host memory); "
+                   "batch: poporon_decode_batch_device, wall time; checked against oracle/rs_oracle.c")
+    out["verified"] = all(v["mismatches"] == 0 for kk, v in out.items() if isinstance(v, dict))
+    return out
+
+
 def call_latency(be, calls=2000):
     """The reference's calling pattern: one codeword per poporon_encode /
     poporon_decode call (include/poporon.h:90-91), host buffers, on the GPU
@@ -1269,6 +1343,9 @@ def main(argv=None):
             gp = general_params(be)
             line["general_params"] = gp
             line["verified"] = line["verified"] and gp["verified"]
+            gw = general_wave(be)
+            line["general_wave"] = gw
+            line["verified"] = line["verified"] and gw["verified"]
     else:
         if "decode_mixed" in line:
             line["decode_mixed"].pop("_kt", None)
