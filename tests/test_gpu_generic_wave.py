@@ -181,3 +181,70 @@ def test_generic_check_and_syndromes_vs_oracle(torch_cuda, params, path, monkeyp
             f, want = o.syndrome(cw[c, :size], cw[c, size:])
             assert bool(gd[c]) == f and bool(gn[c]) == f and (got[c] == want).all(), (size, c)
     h.close()
+
+
+@pytest.mark.parametrize("path", ["wave", "lane"])
+@pytest.mark.parametrize("params", [(8, 0x11D, 1, 1, 100), (4, 0x13, 1, 2, 8), (8, 0x11D, 2000, 37, 32)])
+def test_generic_single_call_edges_vs_oracle(params, path, monkeypatch):
+    """Single calls on the general kernels at the branch edges: external
+    syndromes (own, random, all nn, and a value past the field: refused with
+    the bytes untouched), erasure counts 0 .. nr + 2 with stale slots (past nr
+    on a dirty codeword: refused, Q5; on a clean one: success), shortened
+    sizes 1 and k, against the oracle."""
+    from oracle import Oracle
+    monkeypatch.setenv("POPORON_AMD_GENERIC", path)
+    m, poly, fcr, prim, nr = params
+    nn = (1 << m) - 1
+    k = nn - nr
+    o = Oracle(*params)
+    rng = np.random.default_rng(nr + m + 11)
+    syn = np.zeros(nr, np.uint16)
+    hx = P.Poporon(m, poly, fcr, prim, nr, syndrome=syn)
+    er = P.Erasure(nr, nr + 4)
+    he = P.Poporon(m, poly, fcr, prim, nr, erasure=er)
+    for size in (k, 1):
+        for c in range(24):
+            data = rng.integers(0, nn + 1, size, dtype=np.uint8)
+            par = o.encode(data)
+            cw = np.concatenate([data, par])
+            ne = c % (nr // 2 + 2)
+            if c % 5 == 4:
+                ne = 0  # clean
+            pos = rng.permutation(size + nr)[:ne]
+            cw[pos] ^= rng.integers(1, nn + 1, ne).astype(np.uint8)
+            d, p = cw[:size], cw[size:]
+            # external syndromes (the handle reads the array live)
+            kind = c % 4
+            if kind == 0:
+                syn[:] = o.syndrome(d, p)[1]
+            elif kind == 1:
+                syn[:] = rng.integers(0, nn + 1, nr)
+            elif kind == 2:
+                syn[:] = nn
+            else:
+                syn[:] = o.syndrome(d, p)[1]
+                syn[rng.integers(0, nr)] = nn + 1
+            hx._syn[:] = syn
+            got = hx.decode(d, p)
+            if (syn > nn).any():
+                want = (False, 0, d, p)
+            else:
+                want = o.decode(d, p, ext_syn=syn)
+            assert got[0] == want[0] and got[1] == want[1], (size, c, kind)
+            assert (got[2] == want[2]).all() and (got[3] == want[3]).all(), (size, c, kind)
+            # erasures: count 0 .. nr + 2, stale slots from the previous fill
+            e = c % (nr + 3)
+            slots = rng.integers(0, size + nr, nr + 4).astype(np.uint32)
+            er.set(slots)
+            er.set(slots[:e])
+            got = he.decode(d, p)
+            if e > nr:  # Q5 (undefined in the reference): refused for a dirty codeword, success for a clean one
+                want = (not o.syndrome(d, p)[0], 0, d, p)
+            else:  # count e, the row's nr slots with the stale ones past e (Q2)
+                wok, wcor, wd, wp = o.decode_batch(d[None, :], p[None, :], slots[None, :nr],
+                                                   np.array([e], np.uint32))
+                want = (bool(wok[0]), int(wcor[0]), wd[0], wp[0])
+            assert got[0] == want[0] and got[1] == want[1], (size, c, e)
+            assert (got[2] == want[2]).all() and (got[3] == want[3]).all(), (size, c, e)
+    hx.close()
+    he.close()
