@@ -486,15 +486,18 @@ __device__ __forceinline__ uint32_t gw_xor(uint32_t v)
 
 /* out[i] = v[i - 1] over the four register slots (index i = lane + 64 q);
  * out[0] = first.  DPP wave_shr:1, the slot's carry through lane 63 */
-__device__ __forceinline__ void gw_shift(const uint32_t (&v)[4], uint32_t (&out)[4], uint32_t lane, uint32_t first)
+__device__ __forceinline__ void gw_shift(const uint32_t (&v)[4], uint32_t (&out)[4], uint32_t lane, uint32_t first,
+                                         uint32_t nq)
 {
     uint32_t carry = first;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-        const uint32_t top = (uint32_t)__builtin_amdgcn_readlane((int)v[q], 63);
-        const uint32_t u = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v[q], 0x138, 0xf, 0xf, true);
-        out[q] = lane ? u : carry;
-        carry = top;
+        if ((uint32_t)q < nq) { /* slots past nq hold nothing (uniform) */
+            const uint32_t top = (uint32_t)__builtin_amdgcn_readlane((int)v[q], 63);
+            const uint32_t u = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v[q], 0x138, 0xf, 0xf, true);
+            out[q] = lane ? u : carry;
+            carry = top;
+        }
     }
 }
 
@@ -609,6 +612,7 @@ __device__ bool gw_correct(const GwSmem &sm, GwWave &W, const RsGenParams &P, co
     const uint32_t nr = P.nroots, nn = P.nn, A0 = P.nn, size = P.size;
     const int32_t pad = P.pad;
     const uint8_t *alog = sm.alog, *lg = sm.log, *al2 = sm.al2;
+    const uint32_t nq = (nr + 64u) / 64u; /* register slots holding indices 0 .. nr (uniform) */
     uint32_t lam[4], B[4], Bm[4];
 #pragma unroll
     for (int q = 0; q < 4; ++q)
@@ -625,10 +629,10 @@ __device__ bool gw_correct(const GwSmem &sm, GwWave &W, const RsGenParams &P, co
         gw_sync();
         for (uint32_t e = 0; e < ne; ++e) {
             const uint32_t xl = mod(P.prim * (A0 - 1u - (W.acc[e] + (uint32_t)pad)));
-            gw_shift(lam, Bm, lane, 0u);
+            gw_shift(lam, Bm, lane, 0u, nq);
 #pragma unroll
             for (int q = 0; q < 4; ++q)
-                if (Bm[q] != 0u)
+                if ((uint32_t)q < nq && Bm[q] != 0u)
                     lam[q] ^= al2[xl + lg[Bm[q]]];
         }
     }
@@ -643,7 +647,7 @@ __device__ bool gw_correct(const GwSmem &sm, GwWave &W, const RsGenParams &P, co
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
             const uint32_t i = lane + 64u * q;
-            if (i < r && lam[q] != 0u) {
+            if ((uint32_t)q < nq && i < r && lam[q] != 0u) {
                 const uint32_t sv = W.S[r - i - 1u];
                 if (sv != A0)
                     part ^= al2[lg[lam[q]] + sv];
@@ -651,16 +655,18 @@ __device__ bool gw_correct(const GwSmem &sm, GwWave &W, const RsGenParams &P, co
         }
         const uint32_t disc = lg[gw_xor(part)];
         if (disc == A0) {
-            gw_shift(B, Bm, lane, A0);
+            gw_shift(B, Bm, lane, A0, nq);
 #pragma unroll
             for (int q = 0; q < 4; ++q)
                 B[q] = Bm[q];
             continue;
         }
         const bool lengthen = 2u * L <= r + ne - 1u;
-        gw_shift(B, Bm, lane, A0);
+        gw_shift(B, Bm, lane, A0, nq);
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
+            if ((uint32_t)q >= nq)
+                continue;
             const uint32_t old = lam[q];
             if (Bm[q] != A0)
                 lam[q] = old ^ al2[disc + Bm[q]];
@@ -681,7 +687,7 @@ __device__ bool gw_correct(const GwSmem &sm, GwWave &W, const RsGenParams &P, co
     for (int q = 0; q < 4; ++q) {
         const uint32_t i = lane + 64u * q;
         const uint32_t l = lg[lam[q]];
-        const bool valid = i <= nr;
+        const bool valid = (uint32_t)q < nq && i <= nr;
         if (valid) {
             W.lam[i] = (uint8_t)l;
             W.lamz[i] = l == A0 ? GW_Z : l;
@@ -705,11 +711,14 @@ __device__ bool gw_correct(const GwSmem &sm, GwWave &W, const RsGenParams &P, co
             acc[q] = 1;
             tt[q] = 0;
         }
+        const uint32_t np = (nn + 63u) / 64u; /* slots holding the points 1 .. nn (uniform) */
 #pragma unroll 4
         for (uint32_t j = 1; j <= deg; ++j) {
             const uint32_t lz = W.lamz[j];
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
+                if ((uint32_t)q >= np)
+                    continue;
                 tt[q] += pm[q];
                 tt[q] = tt[q] >= nn ? tt[q] - nn : tt[q];
                 acc[q] ^= al2[lz + tt[q]];
