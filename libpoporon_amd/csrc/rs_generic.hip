@@ -882,7 +882,7 @@ __device__ bool gw_correct(const GwSmem &sm, GwWave &W, const RsGenParams &P, co
 /* Full decode, branch logic of src/decode.c:431-487, one codeword per wave
  * (rsg_decode_k's modes: ext / erasure slots / errors; list mode) */
 template <typename PosT>
-__global__ __launch_bounds__(GW_WG) void rsgw_decode_k(const RsGenTables *__restrict__ T, RsGenParams P,
+__global__ __launch_bounds__(GW_WG, 4) void rsgw_decode_k(const RsGenTables *__restrict__ T, RsGenParams P,
                                                         uint8_t *data, size_t dstride, uint8_t *parity,
                                                         size_t pstride, size_t count,
                                                         const uint16_t *__restrict__ ext, size_t ext_stride,

@@ -1,9 +1,9 @@
 #!/usr/bin/env python3
 """Latency and throughput of every parameter set of the reference's own
 tests (tests/golden/rs_params_golden.npz): single calls (poporon_encode /
-poporon_decode through ctypes, t errors) and device batches of 4,096 and
-65,536 codewords (t errors each), with the CPU oracle's single-thread decode
-time beside them for scale.
+poporon_decode through ctypes, t errors) and device batches of 64, 4,096 and
+65,536 codewords (t errors each), with the reference's own single calls
+(oracle/_ref, the same ctypes path, one host core) beside them.
 
     python tools/general_lat.py [--calls 100]"""
 import argparse
@@ -58,6 +58,19 @@ def main():
         td = (time.perf_counter() - t0) / a.calls
         okfrac = float(np.mean([r[0] for r in res]))  # 0 for two sets: the reference's own failures (oracle)
         row = {"encode_us": round(te * 1e6, 1), "decode_us": round(td * 1e6, 1), "single_ok": okfrac}
+        # the reference itself (oracle/_ref, compiled from /root/reference/src), same calls through ctypes
+        from oracle import Reference, reference_available
+        if reference_available():
+            ref = Reference(m, poly, fcr, prim, nr)
+            t0 = time.perf_counter()
+            for x in msgs:
+                ref.encode(x)
+            row["ref_encode_us"] = round((time.perf_counter() - t0) / a.calls * 1e6, 1)
+            t0 = time.perf_counter()
+            for cw in bad:
+                ref.decode(cw[:k], cw[k:])
+            row["ref_decode_us"] = round((time.perf_counter() - t0) / a.calls * 1e6, 1)
+            ref.close()
         for n in (64, 4096, 65536):
             data = rng.integers(0, nn + 1, (n, k), dtype=np.uint8)
             cw = np.concatenate([data, h.encode_batch(data)], 1)
