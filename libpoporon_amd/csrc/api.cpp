@@ -2263,8 +2263,13 @@ static bool srv_launch(poporon_t *h, uint32_t last)
     if (!g.sstream)
         HIP_OK(hipStreamCreateWithFlags(&g.sstream, hipStreamNonBlocking));
     const uint32_t id = g.srv_id + 1u;
-    RsCorrParams prm = h->corr;
-    HIP_OK(rsk_serve(g.tab, &prm, g.zc_dev, last, id, SRV_IDLE_TICKS, SRV_MAX_TICKS, g.sstream));
+    if (h->fast || h->nrsplit) {
+        RsCorrParams prm = h->corr;
+        HIP_OK(rsk_serve(g.tab, &prm, g.zc_dev, last, id, SRV_IDLE_TICKS, SRV_MAX_TICKS, g.sstream));
+    } else { /* general parameters: one wave, GZ_* payload (rs_generic.hip rsgw_serve_k) */
+        RsGenParams prm = h->gen;
+        HIP_OK(rsgw_serve(g.gtab, &prm, g.zc_dev, last, id, SRV_IDLE_TICKS, SRV_MAX_TICKS, g.sstream));
+    }
     g.srv_id = id;
     g.srv_on = true;
     return true;
@@ -2394,15 +2399,20 @@ EXPORT bool poporon_encode(poporon_t *h, uint8_t *data, size_t size, uint8_t *pa
     /* general parameters: rsgw_encode_k on coherent host memory, the same way */
     if (h->fec_type == PPLN_FEC_RS && h->generic && gen_wave(h, 1, true, size) && ensure_zc(g)) {
         memcpy(g.zc + GZ_DATA, data, size);
-        RsGenParams prm = h->gen;
-        prm.size = (uint32_t)size;
-        const uint32_t seq = ++g.zc_seq;
-        KernelTimer t(g, POPORON_AMD_KERNEL_ENCODE, g.stream);
-        HIP_OK(rsgw_encode(g.gtab, &prm, g.zc_dev + GZ_DATA, size, g.zc_dev + GZ_PAR, nr, 1,
-                           reinterpret_cast<uint32_t *>(g.zc_dev + ZC_FLAG), seq, g.num_cu, g.stream));
-        t.done();
-        if (!zc_wait(g, seq))
-            return false;
+        if (serve_enabled() && !g.timing) {
+            if (!srv_call(h, RS_SRV_ENCODE, (uint32_t)size, 0u))
+                return false;
+        } else {
+            RsGenParams prm = h->gen;
+            prm.size = (uint32_t)size;
+            const uint32_t seq = ++g.zc_seq;
+            KernelTimer t(g, POPORON_AMD_KERNEL_ENCODE, g.stream);
+            HIP_OK(rsgw_encode(g.gtab, &prm, g.zc_dev + GZ_DATA, size, g.zc_dev + GZ_PAR, nr, 1,
+                               reinterpret_cast<uint32_t *>(g.zc_dev + ZC_FLAG), seq, g.num_cu, g.stream));
+            t.done();
+            if (!zc_wait(g, seq))
+                return false;
+        }
         memcpy(parity, g.zc + GZ_PAR, nr);
         return true;
     }
@@ -2545,17 +2555,22 @@ static bool rs_decode_one(poporon_t *h, uint8_t *data, size_t size, uint8_t *par
             if (refuse) {
                 fail("external syndrome > field size: undefined in the reference, refused");
             } else {
-                RsGenParams prm = h->gen;
-                prm.size = (uint32_t)size;
-                prm.pad = (int32_t)(nn - nr - size);
-                const uint32_t seq = ++g.zc_seq;
-                KernelTimer t(g, POPORON_AMD_KERNEL_CORRECT, g.stream);
-                HIP_OK(rsgw_decode(g.gtab, &prm, zd + GZ_DATA, size, zd + GZ_PAR, nr, 1, ext, nr, nullptr, pos32, nr,
-                                   cnt, zd + GZ_OK, zd + GZ_COR, nullptr, nullptr,
-                                   reinterpret_cast<uint32_t *>(zd + ZC_FLAG), seq, g.num_cu, g.stream));
-                t.done();
-                if (!zc_wait(g, seq))
-                    return false;
+                if (serve_enabled() && !g.timing) {
+                    if (!srv_call(h, RS_SRV_DECODE, (uint32_t)size, ext ? 2u : pos32 ? 1u : 0u))
+                        return false;
+                } else {
+                    RsGenParams prm = h->gen;
+                    prm.size = (uint32_t)size;
+                    prm.pad = (int32_t)(nn - nr - size);
+                    const uint32_t seq = ++g.zc_seq;
+                    KernelTimer t(g, POPORON_AMD_KERNEL_CORRECT, g.stream);
+                    HIP_OK(rsgw_decode(g.gtab, &prm, zd + GZ_DATA, size, zd + GZ_PAR, nr, 1, ext, nr, nullptr, pos32,
+                                       nr, cnt, zd + GZ_OK, zd + GZ_COR, nullptr, nullptr,
+                                       reinterpret_cast<uint32_t *>(zd + ZC_FLAG), seq, g.num_cu, g.stream));
+                    t.done();
+                    if (!zc_wait(g, seq))
+                        return false;
+                }
                 memcpy(data, z + GZ_DATA, size);
                 memcpy(parity, z + GZ_PAR, nr);
                 success = z[GZ_OK] != 0;

@@ -506,15 +506,16 @@ __device__ __forceinline__ void gw_shift(const uint32_t (&v)[4], uint32_t (&out)
  * a few us per launch) */
 __device__ __forceinline__ void gw_fill_al2(uint8_t *al2, const uint8_t *alog_lds, uint32_t nn)
 {
-    for (uint32_t x = threadIdx.x; x < GW_AL2; x += GW_WG)
+    for (uint32_t x = threadIdx.x; x < GW_AL2; x += blockDim.x)
         al2[x] = x < nn ? alog_lds[x] : (x < 2u * nn ? alog_lds[x - nn] : (uint8_t)0);
 }
 
 __device__ __forceinline__ void gw_tables(GwSmem &sm, const RsGenTables *__restrict__ T, uint32_t nn)
 {
-    const uint32_t t = threadIdx.x;
-    sm.alog[t] = T->alog[t];
-    sm.log[t] = T->log[t];
+    for (uint32_t t = threadIdx.x; t < 256u; t += blockDim.x) {
+        sm.alog[t] = T->alog[t];
+        sm.log[t] = T->log[t];
+    }
     __syncthreads();
     gw_fill_al2(sm.al2, sm.alog, nn);
 }
@@ -879,19 +880,72 @@ __device__ bool gw_correct(const GwSmem &sm, GwWave &W, const RsGenParams &P, co
     return first_bad == deg;
 }
 
-/* Full decode, branch logic of src/decode.c:431-487, one codeword per wave
- * (rsg_decode_k's modes: ext / erasure slots / errors; list mode) */
+/* One codeword on one wave, branch logic of src/decode.c:431-487: x (the
+ * row's external log-form syndromes) or pos / ne (its erasure slots and
+ * count) or neither; ok / corrected_num to okp / corp (corp may be NULL) */
+template <typename PosT>
+__device__ void gw_decode_one(const GwSmem &sm, GwWave &W, const RsGenParams &P, const GMod &mod, uint32_t lane,
+                              bool qf, uint8_t *d, uint8_t *par, const uint16_t *x, const PosT *pos, uint32_t ne,
+                              uint8_t *okp, uint8_t *corp)
+{
+    const uint32_t nr = P.nroots, A0 = P.nn, size = P.size, total = size + nr;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const uint32_t b = lane + 64u * q;
+        const uint32_t v = b < size ? d[b] : (b < total ? par[b - size] : 0u);
+        const uint32_t m = v & A0;
+        W.cw[b] = (uint8_t)v;
+        W.lr[b] = m ? (uint32_t)sm.log[m] : GW_Z;
+    }
+    uint32_t fixed = 0;
+    bool good;
+    if (x) {
+        bool bad = false, any = false;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const uint32_t i = lane + 64u * q;
+            if (i < nr) {
+                const uint32_t v = x[i];
+                bad |= v > A0;
+                any |= v != A0;
+                W.S[i] = (uint8_t)v;
+                W.sz[i] = v == A0 ? GW_Z : (v & 0xffu);
+            }
+        }
+        bad = __ballot(bad) != 0ull;
+        any = __ballot(any) != 0ull;
+        gw_sync();
+        good = !bad &&
+               (!any || gw_correct<PosT>(sm, W, P, mod, lane, d, par, 0u, (const PosT *)nullptr, false, fixed));
+    } else {
+        gw_sync();
+        const bool dirty = gw_syndromes(sm, W, P, mod, lane, qf);
+        if (pos)
+            good = !dirty || (ne <= nr && gw_correct<PosT>(sm, W, P, mod, lane, d, par, ne, pos, true, fixed));
+        else
+            good = !dirty || gw_correct<PosT>(sm, W, P, mod, lane, d, par, 0u, (const PosT *)nullptr, false, fixed);
+    }
+    if (lane == 0u) {
+        *okp = good ? 1 : 0;
+        if (corp)
+            *corp = (uint8_t)fixed;
+    }
+    gw_sync();
+}
+
+/* Full decode, one codeword per wave (rsg_decode_k's modes: ext / erasure
+ * slots / errors; list mode) */
 template <typename PosT>
 __global__ __launch_bounds__(GW_WG, 4) void rsgw_decode_k(const RsGenTables *__restrict__ T, RsGenParams P,
-                                                        uint8_t *data, size_t dstride, uint8_t *parity,
-                                                        size_t pstride, size_t count,
-                                                        const uint16_t *__restrict__ ext, size_t ext_stride,
-                                                        const PosT *__restrict__ pos, size_t pos_stride,
-                                                        const uint8_t *__restrict__ cntv, uint8_t *__restrict__ ok,
-                                                        uint8_t *__restrict__ corrected,
-                                                        const uint32_t *__restrict__ list,
-                                                        const uint32_t *__restrict__ list_n, uint32_t *flag,
-                                                        uint32_t seq)
+                                                           uint8_t *data, size_t dstride, uint8_t *parity,
+                                                           size_t pstride, size_t count,
+                                                           const uint16_t *__restrict__ ext, size_t ext_stride,
+                                                           const PosT *__restrict__ pos, size_t pos_stride,
+                                                           const uint8_t *__restrict__ cntv, uint8_t *__restrict__ ok,
+                                                           uint8_t *__restrict__ corrected,
+                                                           const uint32_t *__restrict__ list,
+                                                           const uint32_t *__restrict__ list_n, uint32_t *flag,
+                                                           uint32_t seq)
 {
     const size_t n = list ? (size_t)*list_n : count;
     if ((size_t)blockIdx.x * (GW_WG / 64) >= n)
@@ -902,59 +956,12 @@ __global__ __launch_bounds__(GW_WG, 4) void rsgw_decode_k(const RsGenTables *__r
     __syncthreads();
     GwWave &W = sm.w[wave];
     const GMod mod{P.nn, P.magic};
-    const uint32_t nr = P.nroots, A0 = P.nn, size = P.size, total = size + nr;
-    const bool qf = (P.fcr + nr - 1u) * P.prim + A0 - 1u < 65536u;
+    const bool qf = (P.fcr + P.nroots - 1u) * P.prim + P.nn - 1u < 65536u;
     for (size_t e = (size_t)blockIdx.x * (GW_WG / 64) + wave; e < n; e += (size_t)gridDim.x * (GW_WG / 64)) {
         const size_t cw = list ? (size_t)list[e] : e;
-        uint8_t *d = data + cw * dstride;
-        uint8_t *par = parity + cw * pstride;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const uint32_t b = lane + 64u * q;
-            const uint32_t v = b < size ? d[b] : (b < total ? par[b - size] : 0u);
-            const uint32_t m = v & A0;
-            W.cw[b] = (uint8_t)v;
-            W.lr[b] = m ? (uint32_t)sm.log[m] : GW_Z;
-        }
-        uint32_t fixed = 0;
-        bool good;
-        if (ext) {
-            const uint16_t *x = ext + cw * ext_stride;
-            bool bad = false, any = false;
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const uint32_t i = lane + 64u * q;
-                if (i < nr) {
-                    const uint32_t v = x[i];
-                    bad |= v > A0;
-                    any |= v != A0;
-                    W.S[i] = (uint8_t)v;
-                    W.sz[i] = v == A0 ? GW_Z : (v & 0xffu);
-                }
-            }
-            bad = __ballot(bad) != 0ull;
-            any = __ballot(any) != 0ull;
-            gw_sync();
-            good = !bad && (!any || gw_correct<PosT>(sm, W, P, mod, lane, d, par, 0u, (const PosT *)nullptr, false,
-                                                      fixed));
-        } else {
-            gw_sync();
-            const bool dirty = gw_syndromes(sm, W, P, mod, lane, qf);
-            if (pos) {
-                const uint32_t ne = cntv[cw];
-                good = !dirty || (ne <= nr && gw_correct<PosT>(sm, W, P, mod, lane, d, par, ne, pos + cw * pos_stride,
-                                                                true, fixed));
-            } else {
-                good = !dirty ||
-                       gw_correct<PosT>(sm, W, P, mod, lane, d, par, 0u, (const PosT *)nullptr, false, fixed);
-            }
-        }
-        if (lane == 0u) {
-            ok[cw] = good ? 1 : 0;
-            if (corrected)
-                corrected[cw] = (uint8_t)fixed;
-        }
-        gw_sync();
+        gw_decode_one<PosT>(sm, W, P, mod, lane, qf, data + cw * dstride, parity + cw * pstride,
+                            ext ? ext + cw * ext_stride : nullptr, pos ? pos + cw * pos_stride : nullptr,
+                            pos ? (uint32_t)cntv[cw] : 0u, ok + cw, corrected ? corrected + cw : nullptr);
     }
     gw_done(flag, seq);
 }
@@ -1004,96 +1011,84 @@ __global__ __launch_bounds__(GW_WG) void rsgw_check_k(const RsGenTables *__restr
 /* Encode, one message per wave: parity = sum_b d_b Q[size - 1 - b], Q[d] the
  * parity of the message 1 followed by d zeros (RsGenTables::encq, built on
  * the host by the reference's LFSR, src/encode.c:120-143, which is linear
- * in the masked message bytes); lane p (and p + 64 ...) owns parity byte p */
-__global__ __launch_bounds__(GW_WG) void rsgw_encode_k(const RsGenTables *__restrict__ T, RsGenParams P,
-                                                        const uint8_t *__restrict__ data, size_t dstride,
-                                                        uint8_t *__restrict__ parity, size_t pstride, size_t count,
-                                                        uint32_t *flag, uint32_t seq)
+ * in the masked message bytes). */
+
+/* the rows Q[0 .. size) into qs (nr logs each, GW_Z: zero): 16-byte chunks,
+ * up to four per thread issued before any is used (a row per step, one load
+ * at a time, had cost ~0.3 us each) */
+__device__ __forceinline__ void gw_stage_rows(uint16_t *qs, const RsGenTables *__restrict__ T, uint32_t size,
+                                              uint32_t nr)
 {
-    /* single calls and tiny batches of messages longer than their parity:
-     * lanes over the message bytes (nr reductions) rather than over the
-     * parity bytes (size serial steps): RS(255,207) 25 vs 43 us per call,
-     * RS(255,55) 46 vs 31 (profiles/r05_general_lat_auto.log) */
-    const bool by_byte = count <= 64u && P.size > P.nroots;
-    if ((size_t)blockIdx.x * (GW_WG / 64) >= count)
-        return;
-    __shared__ uint8_t al2[GW_AL2];
-    __shared__ uint8_t lg[256];
-    __shared__ uint16_t lr[GW_WG / 64][256];
-    __shared__ uint16_t qs[GW_QS]; /* the rows Q[0 .. size) packed (nr logs each, GW_Z: zero): size + nr <= 255 */
-    __shared__ uint8_t alog[256];
-    const uint32_t t = threadIdx.x, lane = t & 63u, wave = t >> 6;
-    const uint32_t nn = P.nn, A0 = P.nn, nr = P.nroots, size = P.size;
-    lg[t] = T->log[t];
-    alog[t] = T->alog[t];
-    /* 16-byte chunks of the rows, up to four per thread issued before any is
-     * used (a row per step, one load at a time, had cost ~0.3 us each) */
-    {
-        const uint32_t cpr = (nr + 15u) / 16u, nch = size * cpr;
-        for (uint32_t x0 = t; x0 < nch; x0 += 4u * GW_WG) {
-            uint4 v[4];
+    const uint32_t t = threadIdx.x, nt = blockDim.x;
+    const uint32_t cpr = (nr + 15u) / 16u, nch = size * cpr;
+    for (uint32_t x0 = t; x0 < nch; x0 += 4u * nt) {
+        uint4 v[4];
 #pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const uint32_t x = x0 + (uint32_t)k * GW_WG;
-                if (x < nch)
-                    v[k] = *reinterpret_cast<const uint4 *>(T->encq + (x / cpr) * 256u + (x % cpr) * 16u);
-            }
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t x = x0 + (uint32_t)k * nt;
+            if (x < nch)
+                v[k] = *reinterpret_cast<const uint4 *>(T->encq + (x / cpr) * 256u + (x % cpr) * 16u);
+        }
 #pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const uint32_t x = x0 + (uint32_t)k * GW_WG;
-                if (x < nch) {
-                    const uint32_t r = x / cpr, c = x % cpr;
-                    const uint32_t w[4] = {v[k].x, v[k].y, v[k].z, v[k].w};
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t x = x0 + (uint32_t)k * nt;
+            if (x < nch) {
+                const uint32_t r = x / cpr, c = x % cpr;
+                const uint32_t w[4] = {v[k].x, v[k].y, v[k].z, v[k].w};
 #pragma unroll
-                    for (int j = 0; j < 16; ++j) {
-                        const uint32_t pp = c * 16u + (uint32_t)j;
-                        const uint32_t b = (w[j >> 2] >> (8 * (j & 3))) & 0xffu;
-                        if (pp < nr)
-                            qs[r * nr + pp] = b == 0xffu ? GW_Z : b;
-                    }
+                for (int j = 0; j < 16; ++j) {
+                    const uint32_t pp = c * 16u + (uint32_t)j;
+                    const uint32_t b = (w[j >> 2] >> (8 * (j & 3))) & 0xffu;
+                    if (pp < nr)
+                        qs[r * nr + pp] = b == 0xffu ? GW_Z : b;
                 }
             }
         }
     }
-    __syncthreads();
-    gw_fill_al2(al2, alog, nn);
-    __syncthreads();
-    for (size_t e = (size_t)blockIdx.x * (GW_WG / 64) + wave; e < count; e += (size_t)gridDim.x * (GW_WG / 64)) {
-        const uint8_t *d = data + e * dstride;
+}
+
+/* one message on one wave (lr: the wave's 256-entry log row); by_byte: lanes
+ * over the message bytes, one XOR reduction per parity byte (single calls of
+ * messages longer than their parity: RS(255,207) 25 vs 43 us per call,
+ * RS(255,55) 46 vs 31, profiles/r05_general_lat_auto.log); else lane p (and
+ * p + 64 ...) owns parity byte p over size serial steps */
+__device__ __forceinline__ void gw_encode_one(const uint8_t *al2, const uint8_t *lg, uint16_t *lr, const uint16_t *qs,
+                                              const RsGenParams &P, uint32_t lane, bool by_byte, const uint8_t *d,
+                                              uint8_t *out)
+{
+    const uint32_t A0 = P.nn, nr = P.nroots, size = P.size;
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const uint32_t b = lane + 64u * q;
-            if (b < size) {
-                const uint32_t m = (uint32_t)d[b] & A0;
-                lr[wave][b] = m ? (uint32_t)lg[m] : GW_Z;
-            }
+    for (int q = 0; q < 4; ++q) {
+        const uint32_t b = lane + 64u * q;
+        if (b < size) {
+            const uint32_t m = (uint32_t)d[b] & A0;
+            lr[b] = m ? (uint32_t)lg[m] : GW_Z;
         }
-        gw_sync();
-        uint32_t acc[4] = {0, 0, 0, 0};
-        const uint32_t nq = (nr + 63u) / 64u;
-        if (by_byte) {
-            /* lanes over the message bytes (b = lane + 64 k), one XOR reduction
-             * per parity byte: nr short steps instead of size serial ones */
-            uint32_t lb[4], rb[4];
+    }
+    gw_sync();
+    uint32_t acc[4] = {0, 0, 0, 0};
+    const uint32_t nq = (nr + 63u) / 64u;
+    if (by_byte) {
+        uint32_t lb[4], rb[4];
 #pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const uint32_t b = lane + 64u * k;
-                lb[k] = b < size ? (uint32_t)lr[wave][b] : GW_Z;
-                rb[k] = b < size ? (size - 1u - b) * nr : 0u;
-            }
-            for (uint32_t p = 0; p < nr; ++p) {
-                uint32_t x = 0;
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t b = lane + 64u * k;
+            lb[k] = b < size ? (uint32_t)lr[b] : GW_Z;
+            rb[k] = b < size ? (size - 1u - b) * nr : 0u;
+        }
+        for (uint32_t p = 0; p < nr; ++p) {
+            uint32_t x = 0;
 #pragma unroll
-                for (int k = 0; k < 4; ++k)
-                    x ^= al2[lb[k] + qs[rb[k] + p]];
-                x = gw_xor(x);
-                if ((p & 63u) == lane)
-                    acc[p >> 6] = x;
-            }
-        } else
+            for (int k = 0; k < 4; ++k)
+                x ^= al2[lb[k] + qs[rb[k] + p]];
+            x = gw_xor(x);
+            if ((p & 63u) == lane)
+                acc[p >> 6] = x;
+        }
+    } else {
 #pragma unroll 4
         for (uint32_t b = 0; b < size; ++b) {
-            const uint32_t l = lr[wave][b]; /* zero byte or zero entry: a sentinel sum, al2's zero part */
+            const uint32_t l = lr[b]; /* zero byte or zero entry: a sentinel sum, al2's zero part */
             const uint16_t *row = qs + (size - 1u - b) * nr;
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
@@ -1102,16 +1097,122 @@ __global__ __launch_bounds__(GW_WG) void rsgw_encode_k(const RsGenTables *__rest
                     acc[q] ^= al2[l + row[p]];
             }
         }
-        uint8_t *out = parity + e * pstride;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const uint32_t p = lane + 64u * q;
-            if (p < nr)
-                out[p] = (uint8_t)acc[q];
-        }
-        gw_sync();
     }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const uint32_t p = lane + 64u * q;
+        if (p < nr)
+            out[p] = (uint8_t)acc[q];
+    }
+    gw_sync();
+}
+
+__global__ __launch_bounds__(GW_WG) void rsgw_encode_k(const RsGenTables *__restrict__ T, RsGenParams P,
+                                                        const uint8_t *__restrict__ data, size_t dstride,
+                                                        uint8_t *__restrict__ parity, size_t pstride, size_t count,
+                                                        uint32_t *flag, uint32_t seq)
+{
+    const bool by_byte = count <= 64u && P.size > P.nroots; /* single calls and tiny batches: latency */
+    if ((size_t)blockIdx.x * (GW_WG / 64) >= count)
+        return;
+    __shared__ uint8_t al2[GW_AL2];
+    __shared__ uint8_t lg[256];
+    __shared__ uint16_t lr[GW_WG / 64][256];
+    __shared__ uint16_t qs[GW_QS]; /* size + nr <= 255 */
+    __shared__ uint8_t alog[256];
+    const uint32_t t = threadIdx.x, lane = t & 63u, wave = t >> 6;
+    lg[t] = T->log[t];
+    alog[t] = T->alog[t];
+    gw_stage_rows(qs, T, P.size, P.nroots);
+    __syncthreads();
+    gw_fill_al2(al2, alog, P.nn);
+    __syncthreads();
+    for (size_t e = (size_t)blockIdx.x * (GW_WG / 64) + wave; e < count; e += (size_t)gridDim.x * (GW_WG / 64))
+        gw_encode_one(al2, lg, lr[wave], qs, P, lane, by_byte, data + e * dstride, parity + e * pstride);
     gw_done(flag, seq);
+}
+
+/*
+ * rsgw_serve_k: the general-parameter single-call server, rs_serve_k's
+ * protocol (rs_single.hip) with one wave: it stays resident between
+ * poporon_encode / poporon_decode calls of a general-parameter handle and
+ * serves them from the handle's coherent host buffer (GZ_* payload, ZC_REQ /
+ * ZC_FLAG / ZC_EXITED words), so a call costs no kernel launch.  Lane 0
+ * polls the request word; encode stages the request's rows Q[0 .. size) and
+ * runs gw_encode_one, decode gw_decode_one in the request's mode (0 errors,
+ * 1 u32 erasure slots, 2 external syndromes); then the sequence word to
+ * ZC_FLAG with a system-scope release.  It leaves after idle_ticks without a
+ * request, after max_ticks in all, or at RS_SRV_STOP, storing its id to
+ * ZC_EXITED (api.cpp srv_call relaunches for a request it did not see).
+ */
+__global__ __launch_bounds__(64) void rsgw_serve_k(const RsGenTables *__restrict__ T, RsGenParams P, uint8_t *zc,
+                                                    uint32_t last, uint32_t id, uint64_t idle_ticks,
+                                                    uint64_t max_ticks)
+{
+    __shared__ GwSmem sm;
+    __shared__ uint16_t qs[GW_QS];
+    __shared__ uint32_t cmd[4]; /* seq, op (0: leave), size, mode */
+    const uint32_t lane = threadIdx.x;
+    gw_tables(sm, T, P.nn);
+    __syncthreads();
+    GwWave &W = sm.w[0];
+    const GMod mod{P.nn, P.magic};
+    const bool qf = (P.fcr + P.nroots - 1u) * P.prim + P.nn - 1u < 65536u;
+    uint32_t *req = reinterpret_cast<uint32_t *>(zc + ZC_REQ);
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    uint64_t idle0 = t0;
+    uint32_t staged = 0; /* message size whose rows Q[0 .. size) are in qs (0: none) */
+    for (;;) {
+        if (lane == 0) {
+            uint32_t r = last, op = 0;
+            for (;;) {
+                r = __hip_atomic_load(req, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+                if (r != last) {
+                    op = ZC_REQ_OP(r);
+                    cmd[2] = ZC_REQ_SIZE(r);
+                    cmd[3] = ZC_REQ_MODE(r);
+                    break;
+                }
+                const uint64_t now = __builtin_amdgcn_s_memrealtime();
+                if (now - idle0 > idle_ticks || now - t0 > max_ticks)
+                    break; /* op = 0: leave */
+                __builtin_amdgcn_s_sleep(1);
+            }
+            cmd[0] = r;
+            cmd[1] = op;
+        }
+        __syncthreads();
+        const uint32_t seq = cmd[0], op = cmd[1], size = cmd[2], mode = cmd[3];
+        if ((op != RS_SRV_ENCODE && op != RS_SRV_DECODE) || size == 0u || size + P.nroots > P.nn)
+            break; /* uniform: idle, lifetime, RS_SRV_STOP; a malformed request also ends the launch */
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, ""); /* the payload's loads: after the request */
+        RsGenParams Q = P;
+        Q.size = size;
+        Q.pad = (int32_t)(P.nn - P.nroots - size);
+        if (op == RS_SRV_ENCODE) {
+            if (size != staged) { /* the rows stay staged for the next request of this size */
+                gw_stage_rows(qs, T, size, P.nroots);
+                __syncthreads();
+                staged = size;
+            }
+            gw_encode_one(sm.al2, sm.log, W.lr, qs, Q, lane, size > P.nroots, zc + GZ_DATA, zc + GZ_PAR);
+        } else {
+            gw_decode_one<uint32_t>(sm, W, Q, mod, lane, qf, zc + GZ_DATA, zc + GZ_PAR,
+                                    mode == 2u ? reinterpret_cast<const uint16_t *>(zc + GZ_EXT) : nullptr,
+                                    mode == 1u ? reinterpret_cast<const uint32_t *>(zc + GZ_POS) : nullptr,
+                                    mode == 1u ? (uint32_t)zc[GZ_CNT] : 0u, zc + GZ_OK, zc + GZ_COR);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (lane == 0)
+            __hip_atomic_store(reinterpret_cast<uint32_t *>(zc + ZC_FLAG), seq, __ATOMIC_RELEASE,
+                               __HIP_MEMORY_SCOPE_SYSTEM);
+        last = seq;
+        idle0 = __builtin_amdgcn_s_memrealtime();
+    }
+    if (lane == 0)
+        __hip_atomic_store(reinterpret_cast<uint32_t *>(zc + ZC_EXITED), id, __ATOMIC_RELEASE,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 /* ------------------------------------------------------------------------ */
@@ -1250,5 +1351,13 @@ extern "C" hipError_t rsgw_check(const RsGenTables *tab, const RsGenParams *prm,
         return hipSuccess;
     RS_LAUNCH(rsgw_check_k, gw_grid(count, num_cu), dim3(GW_WG), 0, stream, tab, *prm, data, dstride, parity, pstride,
               count, dirty, syn, syn_stride);
+    return hipGetLastError();
+}
+
+extern "C" hipError_t rsgw_serve(const RsGenTables *tab, const RsGenParams *prm, uint8_t *zc_dev, uint32_t last,
+                                 uint32_t id, uint64_t idle_ticks, uint64_t max_ticks, hipStream_t stream)
+{
+    hipLaunchKernelGGL(rsgw_serve_k, dim3(1), dim3(64), 0, stream, tab, *prm, zc_dev, last, id, idle_ticks,
+                       max_ticks);
     return hipGetLastError();
 }

@@ -248,3 +248,54 @@ def test_generic_single_call_edges_vs_oracle(params, path, monkeypatch):
             assert (got[2] == want[2]).all() and (got[3] == want[3]).all(), (size, c, e)
     hx.close()
     he.close()
+
+
+@pytest.mark.parametrize("params", [(4, 0x13, 1, 2, 8), (8, 0x11D, 1, 1, 100), (7, 0x89, 1, 1, 20)])
+def test_generic_single_call_server_vs_oracle(params):
+    """The general-parameter single-call server (rsgw_serve_k): calls spaced
+    around its 1 ms idle limit (it leaves and is launched again), device
+    batches and synchronisations in between, a second general handle and an
+    RS(255,223) handle (rs_serve_k) serving at the same time, the per-call
+    launch path (kernel timing on) interleaved, shortened sizes (the staged
+    encode rows change with the size), and a close that stops a live server
+    -- every result equal to the oracle's."""
+    import time
+
+    import torch
+    from oracle import Oracle
+    m, poly, fcr, prim, nr = params
+    nn = (1 << m) - 1
+    k = nn - nr
+    o, od = Oracle(*params), Oracle()
+    h, h2, hd = P.Poporon(*params), P.Poporon(*params), P.Poporon.default()
+    rng = np.random.default_rng(nr * 3 + m)
+    for c in range(40):
+        if c % 3 == 0:
+            time.sleep([0.0, 0.0009, 0.0011, 0.003][(c // 3) % 4])
+        if c % 8 == 5:
+            torch.cuda.synchronize()
+        size = k if c % 4 else int(rng.integers(1, k + 1))
+        data = rng.integers(0, nn + 1, size, dtype=np.uint8)
+        want = o.encode(data)
+        hh = h if c % 2 else h2
+        timing = c % 5 == 3
+        hh.timing(timing)  # kernel timing on: one launch per call instead of the server
+        if c % 8 == 6:
+            bd = np.tile(data, (3, 1))
+            okb, corb, db, pb = hh.decode_batch(bd, np.tile(want, (3, 1)))
+            assert okb.all() and (db == bd).all()
+        assert (hh.encode(data) == want).all(), c
+        cw = np.concatenate([data, want])
+        ne = int(rng.integers(0, nr // 2 + 1))
+        cw[rng.permutation(size + nr)[:ne]] ^= rng.integers(1, nn + 1, ne).astype(np.uint8)
+        got = hh.decode(cw[:size], cw[size:])
+        wok, wn, wd, wp = o.decode(cw[:size], cw[size:])
+        assert got[0] == wok and got[1] == wn and (got[2] == wd).all() and (got[3] == wp).all(), c
+        hh.timing(False)
+        md = rng.integers(0, 256, 223, dtype=np.uint8)
+        assert (hd.encode(md) == od.encode(md)).all(), c
+    h.close()  # asks its live server to leave
+    data = rng.integers(0, nn + 1, k, dtype=np.uint8)
+    assert (h2.encode(data) == o.encode(data)).all()
+    h2.close()
+    hd.close()
