@@ -434,8 +434,7 @@ struct GwWave {
     uint16_t lr[256];   /* log of each masked byte (GW_Z: zero) */
     uint8_t S[256];     /* syndromes, log form (nn: zero) */
     uint16_t sz[256];   /* the same, GW_Z for zero */
-    uint8_t lam[256];   /* locator, log form */
-    uint16_t lamz[256];
+    uint16_t lamz[256]; /* locator, log form, GW_Z for zero */
     uint16_t omz[256];  /* Omega, log form, GW_Z for zero */
     uint16_t lgm[256];  /* per root: log of its magnitude (0xffff: zero) ... */
     uint16_t lx[256];   /* ... and nn - 1 - its location (the re-syndrome check's factor) */
@@ -689,10 +688,8 @@ __device__ bool gw_correct(const GwSmem &sm, GwWave &W, const RsGenParams &P, co
         const uint32_t i = lane + 64u * q;
         const uint32_t l = lg[lam[q]];
         const bool valid = (uint32_t)q < nq && i <= nr;
-        if (valid) {
-            W.lam[i] = (uint8_t)l;
+        if (valid)
             W.lamz[i] = l == A0 ? GW_Z : l;
-        }
         const uint64_t m = __ballot(valid && l != A0);
         if (m)
             deg = 64u * q + 63u - (uint32_t)__clzll((long long)m);
