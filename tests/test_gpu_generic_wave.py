@@ -299,3 +299,45 @@ def test_generic_single_call_server_vs_oracle(params):
     assert (h2.encode(data) == o.encode(data)).all()
     h2.close()
     hd.close()
+
+
+@pytest.mark.parametrize("params", [(8, 0x11D, 1, 1, 100), (4, 0x13, 1, 2, 8), (7, 0x89, 1, 1, 20),
+                                    (6, 0x43, 1, 1, 10)])
+def test_generic_large_batch_round_trip(torch_cuda, params):
+    """Large device batches on the default routing (one codeword per wave for
+    long codes, per lane for short ones past 16,384 codewords): 2^18 rows
+    encoded, t random errors each, decoded -- every row back to the encoded
+    one with ok = 1 and corrected_num = t (a size-independent property), and
+    every 1024th row equal to the oracle's encode and decode."""
+    from oracle import Oracle
+    torch = torch_cuda
+    m, poly, fcr, prim, nr = params
+    nn = (1 << m) - 1
+    k, t = nn - nr, nr // 2
+    n = 1 << 18
+    o, h = Oracle(*params), P.Poporon(*params)
+    rng = np.random.default_rng(nn + nr)
+    data = rng.integers(0, nn + 1, (n, k), dtype=np.uint8)
+    rows = torch.zeros((n, nn), dtype=torch.uint8, device="cuda")
+    rows[:, :k] = torch.from_numpy(data).cuda()
+    s = torch.cuda.current_stream().cuda_stream
+    b = rows.data_ptr()
+    h.encode_batch_device(b, nn, b + k, nn, k, n, s)
+    torch.cuda.synchronize()
+    clean = rows.cpu().numpy()
+    idx = np.arange(0, n, 1024)
+    assert (clean[idx, k:] == o.encode_batch(data[idx])).all()
+    pos = np.argsort(rng.random((n, nn)), axis=1)[:, :t]
+    bad = clean.copy()
+    np.bitwise_xor.at(bad, (np.arange(n)[:, None], pos), rng.integers(1, nn + 1, (n, t), dtype=np.uint8))
+    rows.copy_(torch.from_numpy(bad).cuda())
+    ok = torch.zeros(n, dtype=torch.uint8, device="cuda")
+    cor = torch.zeros(n, dtype=torch.uint8, device="cuda")
+    h.decode_batch_device(b, nn, b + k, nn, k, n, ok.data_ptr(), cor.data_ptr(), stream=s)
+    torch.cuda.synchronize()
+    got = rows.cpu().numpy()
+    assert bool((ok == 1).all()) and bool((cor == t).all())
+    assert (got == clean).all()
+    ook, ocor, od, op = o.decode_batch(bad[idx, :k], bad[idx, k:])
+    assert (ook == 1).all() and (ocor == t).all() and (od == clean[idx, :k]).all() and (op == clean[idx, k:]).all()
+    h.close()
