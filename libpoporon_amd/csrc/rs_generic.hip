@@ -13,8 +13,14 @@
  *                  Forney, re-syndrome check, apply     src/decode.c:17-230
  *                  branch logic (ext. syndrome/erasure) src/decode.c:431-487
  *   rsg_check_k    "any syndrome nonzero" only
+ * in two families:
+ *   rsg_*    one codeword per lane (large batches of short codes), below;
+ *   rsgw_*   one codeword per wave (single calls, small batches, long codes,
+ *            the split decode's lists) and rsgw_serve_k, the single-call
+ *            server of general-parameter handles: after rsg_check_k.
+ * api.cpp gen_wave() picks the family; both give the same bytes.
  *
- * One codeword per lane.  Every per-codeword array (syndromes, locator, B,
+ * Per lane: every per-codeword array (syndromes, locator, B,
  * Omega, roots, locations, magnitudes; num_roots + 1 bytes each) lives in
  * LDS laid out [index][lane], so lanes of a wave touch consecutive bytes.
  * With m <= 8 every field element and every log (A0 = 2^m - 1 is the log of
