@@ -1,6 +1,10 @@
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/tests_all.log 2>&1
-rc=$?; echo "rc=$rc"; tail -1 gpurun_out/tests_all.log
+timeout -k 10 900 python -u bench.py > gpurun_out/bench_final.log 2>&1
+rc=$?; echo "rc=$rc"; python3 -c "
+import json
+l=[x for x in open('gpurun_out/bench_final.log') if x.startswith('{')][-1]
+d=json.loads(l); print(d['value'], d['ms_per_step'], d['verified'], d['roofline']['frac'], d['roofline']['traffic'], d.get('traffic_source'))
+"
 exit $rc
