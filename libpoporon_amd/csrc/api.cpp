@@ -22,6 +22,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <new>
 #include <string>
 #include <thread>
@@ -149,6 +150,13 @@ struct GpuCtx {
     uint32_t srv_id = 0;
     uint32_t srv_seq = 0; /* request words of the server (its own count: zc_seq also moves without it) */
     size_t stage_cap = 0;
+    /* device registry (dev_register): batch_open while a batch call of this
+     * handle is launching, then batch_ev (recorded behind its launches) until
+     * the batch has run; other handles' servers stay off meanwhile */
+    bool registered = false;
+    bool batch_open = false;
+    bool batch_ev_live = false;
+    hipEvent_t batch_ev = nullptr;
     /* host-batch pipeline: PIPE_SLOTS chunks in flight, one stream each */
     struct PipeSlot {
         hipStream_t stream = nullptr;
@@ -842,6 +850,108 @@ static uint32_t srv_word(GpuCtx &g, uint32_t prev, uint32_t op, uint32_t size, u
     return w;
 }
 
+/* Scoped switch to the handle's device; restores the caller's device. */
+struct DeviceGuard {
+    int prev = -1;
+    bool ok = false;
+    explicit DeviceGuard(int dev)
+    {
+        if (hipGetDevice(&prev) != hipSuccess)
+            prev = -1;
+        ok = hipSetDevice(dev) == hipSuccess;
+    }
+    ~DeviceGuard()
+    {
+        if (prev >= 0)
+            (void)hipSetDevice(prev);
+    }
+};
+
+/* ------------------------------------------------------------------------ */
+/* Handles per device: a batch call and other handles' single-call servers   */
+/* ------------------------------------------------------------------------ */
+
+/* A resident single-call server (rs_serve_k / rsgw_serve_k) holds one CU's
+ * LDS; a persistent batch grid (rs_lfsr_k: one 128-160 KB workgroup per CU)
+ * launched beside it waits for that CU until the server leaves (its idle
+ * limit, 1 ms, or 0.5 s while its handle keeps calling).  A batch call stops
+ * its own handle's server (srv_stop); the registry below makes the servers of
+ * the other handles on the device leave too (yield_servers bumps their
+ * ZC_YIELD word, which every server polls with its request word), and keeps
+ * them from relaunching while the batch has not run (srv_may_launch): such a
+ * single call is served by one launch instead (rs_dec1_k / rs_enc1_k /
+ * rsgw_*_k), a kernel that ends on its own.  The reference's handles share
+ * nothing (src/poporon.c, no globals); this keeps a handle's batch
+ * throughput independent of another thread's single calls. */
+#define MAX_DEVS 64
+struct DevRegistry {
+    std::mutex mu;
+    std::vector<GpuCtx *> ctx;
+};
+static DevRegistry g_devs[MAX_DEVS];
+
+static void dev_register(GpuCtx &g)
+{
+    if (g.registered || g.device < 0 || g.device >= MAX_DEVS)
+        return;
+    std::lock_guard<std::mutex> lk(g_devs[g.device].mu);
+    g_devs[g.device].ctx.push_back(&g);
+    g.registered = true;
+}
+
+static void dev_unregister(GpuCtx &g)
+{
+    if (!g.registered)
+        return;
+    DevRegistry &r = g_devs[g.device];
+    std::lock_guard<std::mutex> lk(r.mu);
+    r.ctx.erase(std::remove(r.ctx.begin(), r.ctx.end(), &g), r.ctx.end());
+    g.registered = false;
+}
+
+/* batch_enter: with other handles on the device, mark this batch open and
+ * ask their servers to leave */
+static void yield_servers(GpuCtx &g)
+{
+    if (!g.registered)
+        return;
+    DevRegistry &r = g_devs[g.device];
+    std::lock_guard<std::mutex> lk(r.mu);
+    if (r.ctx.size() < 2)
+        return;
+    g.batch_open = true;
+    for (GpuCtx *x : r.ctx)
+        if (x != &g && x->zc) {
+            volatile uint32_t *y = reinterpret_cast<volatile uint32_t *>(x->zc + ZC_YIELD);
+            *y = *y + 1u;
+        }
+}
+
+/* the end of a batch call: its completion event behind its launches on
+ * `stream` (synchronous calls: none) */
+static void batch_exit(GpuCtx &g, hipStream_t stream, bool sync)
+{
+    if (!g.batch_open)
+        return;
+    DeviceGuard dg(g.device);
+    std::lock_guard<std::mutex> lk(g_devs[g.device].mu);
+    g.batch_open = false;
+    if (sync)
+        return;
+    if (!g.batch_ev && hipEventCreateWithFlags(&g.batch_ev, hipEventDisableTiming) != hipSuccess) {
+        g.batch_ev = nullptr;
+        return;
+    }
+    g.batch_ev_live = hipEventRecord(g.batch_ev, stream) == hipSuccess;
+}
+
+struct BatchScope {
+    GpuCtx &g;
+    hipStream_t stream;
+    bool sync;
+    ~BatchScope() { batch_exit(g, stream, sync); }
+};
+
 /* Frees whatever the context holds, ready or not: a gpu_init that failed
  * half-way leaves a stream or tables behind, and they go here so that the
  * next call retries from scratch. */
@@ -849,18 +959,21 @@ static void gpu_release(GpuCtx &g)
 {
     const int dev = g.device;
     const bool any = g.ready || g.stream || g.sstream || g.tab || g.gtab || g.rem || g.stage || g.hstage || g.zc ||
-                     g.rem_done ||
+                     g.rem_done || g.registered || g.batch_ev ||
                      g.pipe[0].stream || g.pipe[1].stream || g.pipe[2].stream;
     if (!any || dev < 0) {
         g = GpuCtx();
         g.device = dev;
         return;
     }
+    dev_unregister(g); /* no other handle touches g.zc or the batch state from here on */
     int prev = -1;
     (void)hipGetDevice(&prev);
     (void)hipSetDevice(dev);
     if (g.stream)
         (void)hipStreamSynchronize(g.stream);
+    if (g.batch_ev)
+        (void)hipEventDestroy(g.batch_ev);
     if (g.rem_done) {
         (void)hipEventSynchronize(g.rem_done);
         (void)hipEventDestroy(g.rem_done);
@@ -951,22 +1064,6 @@ EXPORT int poporon_amd_device_count(void)
 
 EXPORT bool poporon_amd_supported(const poporon_t *h) { return h && h->supported; }
 
-/* Scoped switch to the handle's device; restores the caller's device. */
-struct DeviceGuard {
-    int prev = -1;
-    bool ok = false;
-    explicit DeviceGuard(int dev)
-    {
-        if (hipGetDevice(&prev) != hipSuccess)
-            prev = -1;
-        ok = hipSetDevice(dev) == hipSuccess;
-    }
-    ~DeviceGuard()
-    {
-        if (prev >= 0)
-            (void)hipSetDevice(prev);
-    }
-};
 
 EXPORT bool poporon_amd_set_device(poporon_t *h, int device)
 {
@@ -1006,7 +1103,10 @@ static bool srv_stop(poporon_t *h);
  * handle beside the batch's kernels */
 static bool batch_enter(poporon_t *h)
 {
-    return gpu_init(h) && srv_stop(h);
+    if (!gpu_init(h) || !srv_stop(h))
+        return false;
+    yield_servers(h->gpu);
+    return true;
 }
 
 static bool gpu_init_steps(poporon_t *h)
@@ -1049,6 +1149,7 @@ static bool gpu_init_steps(poporon_t *h)
         }
     }
     g.ready = true;
+    dev_register(g);
     return true;
 }
 
@@ -1299,7 +1400,9 @@ static bool launch_encode(poporon_t *h, const uint8_t *d_data, size_t ds, uint8_
         HIP_OK(rsk_encode1(h->gpu.tab, d_data, d_par, (uint32_t)size, nullptr, 0, s));
     } else if (h->fast) {
         HIP_OK(rsk_encode(h->gpu.tab, d_data, ds, d_par, ps, (uint32_t)size, count, h->gpu.num_cu, s));
-    } else if (h->lfsr_nr && count == 1 && size <= 255u - h->rs->num_roots) { /* one codeword: the whole workgroup */
+    } else if (h->nrsplit && count == 1 && size <= 255u - h->rs->num_roots) {
+        /* one codeword: the whole workgroup (rs_enc1_k reads exp2 / log, which
+         * build_decode_tables fills only for nrsplit codes) */
         HIP_OK(rsk_encode1_nr(h->gpu.tab, d_data, d_par, (uint32_t)size, h->rs->num_roots, nullptr, 0u, s));
     } else if (h->lfsr_nr) {
         HIP_OK(rsk_encode_nr(h->gpu.tab, d_data, ds, d_par, ps, (uint32_t)size, count, h->rs->num_roots,
@@ -1672,6 +1775,7 @@ EXPORT bool poporon_check_batch_device(poporon_t *h, const uint8_t *d_data, size
         return fail("size %zu outside [1, %u]", size, (unsigned)kmax(h));
     if (!batch_enter(h))
         return false;
+    BatchScope bsc{h->gpu, (hipStream_t)stream, false};
     DeviceGuard dg(h->gpu.device);
     hipStream_t s = (hipStream_t)stream;
     KernelTimer t(h->gpu, POPORON_AMD_KERNEL_CHECK, s);
@@ -1710,6 +1814,7 @@ EXPORT bool poporon_syndrome_batch_device(poporon_t *h, const uint8_t *d_data, s
         return fail("size %zu outside [1, %u]", size, (unsigned)kmax(h));
     if (!batch_enter(h))
         return false;
+    BatchScope bsc{h->gpu, (hipStream_t)stream, false};
     DeviceGuard dg(h->gpu.device);
     hipStream_t s = (hipStream_t)stream;
     if (h->nrsplit) { /* fewer roots: the LFSR kernel's npar syndromes, then their logs */
@@ -1759,6 +1864,7 @@ EXPORT bool poporon_encode_batch_device(poporon_t *h, const uint8_t *d_data, siz
         return false;
     if (!batch_enter(h))
         return false;
+    BatchScope bsc{h->gpu, (hipStream_t)stream, false};
     DeviceGuard dg(h->gpu.device);
     return launch_encode(h, d_data, data_stride, d_parity, parity_stride, size, count, (hipStream_t)stream);
 }
@@ -1776,6 +1882,7 @@ EXPORT bool poporon_decode_batch_device(poporon_t *h, uint8_t *d_data, size_t da
         return fail("decode size %zu outside [1, %u]", size, (unsigned)kmax(h));
     if (!batch_enter(h))
         return false;
+    BatchScope bsc{h->gpu, (hipStream_t)stream, false};
     DeviceGuard dg(h->gpu.device);
     return launch_decode(h, d_data, data_stride, d_parity, parity_stride, size, count, nullptr, 0, d_positions,
                          nullptr, positions_stride, d_counts, d_ok, d_corrected, (hipStream_t)stream);
@@ -1796,6 +1903,7 @@ EXPORT bool poporon_decode_batch_syndrome_device(poporon_t *h, uint8_t *d_data, 
         return fail("decode size %zu outside [1, %u]", size, (unsigned)kmax(h));
     if (!batch_enter(h))
         return false;
+    BatchScope bsc{h->gpu, (hipStream_t)stream, false};
     DeviceGuard dg(h->gpu.device);
     return launch_decode(h, d_data, data_stride, d_parity, parity_stride, size, count, d_syndromes, syndrome_stride,
                          nullptr, nullptr, 0, nullptr, d_ok, d_corrected, (hipStream_t)stream);
@@ -1886,6 +1994,7 @@ EXPORT bool poporon_encode_batch(poporon_t *h, const uint8_t *data, size_t data_
         return false;
     if (!batch_enter(h))
         return false;
+    BatchScope bsc{h->gpu, nullptr, true};
     DeviceGuard dg(h->gpu.device);
     GpuCtx &g = h->gpu;
     const size_t nr = par_bytes(h);
@@ -1941,6 +2050,7 @@ EXPORT bool poporon_decode_batch(poporon_t *h, uint8_t *data, size_t data_stride
         return fail("decode size %zu outside [1, %u]", size, (unsigned)kmax(h));
     if (!batch_enter(h))
         return false;
+    BatchScope bsc{h->gpu, nullptr, true};
     DeviceGuard dg(h->gpu.device);
     GpuCtx &g = h->gpu;
     const size_t nr = par_bytes(h);
@@ -2195,15 +2305,38 @@ static bool ensure_zc(GpuCtx &g)
 {
     if (!g.zc) {
         void *dp = nullptr;
-        if (hipHostMalloc((void **)&g.zc, ZC_BYTES, hipHostMallocCoherent) == hipSuccess &&
-            hipHostGetDevicePointer(&dp, g.zc, 0) == hipSuccess) {
+        uint8_t *hp = nullptr;
+        if (hipHostMalloc((void **)&hp, ZC_BYTES, hipHostMallocCoherent) == hipSuccess &&
+            hipHostGetDevicePointer(&dp, hp, 0) == hipSuccess) {
+            memset(hp, 0, ZC_BYTES);
             g.zc_dev = (uint8_t *)dp;
-            memset(g.zc, 0, ZC_BYTES);
         } else {
             (void)hipGetLastError();
         }
+        if (hp) { /* published under the registry lock: yield_servers writes other handles' buffers */
+            if (g.registered) {
+                std::lock_guard<std::mutex> lk(g_devs[g.device].mu);
+                g.zc = hp;
+            } else {
+                g.zc = hp;
+            }
+        }
     }
     return g.zc_dev != nullptr;
+}
+
+/* Next completion word of a single-call launch (never 0), with ZC_FLAG
+ * cleared first: the server answers with request words from its own counter
+ * (srv_seq), so the word it left there could equal the next zc_seq and
+ * zc_wait would return before this launch wrote anything */
+static uint32_t zc_arm(GpuCtx &g)
+{
+    *reinterpret_cast<volatile uint32_t *>(g.zc + ZC_FLAG) = 0u;
+    std::atomic_thread_fence(std::memory_order_seq_cst);
+    uint32_t s = ++g.zc_seq;
+    if (s == 0u)
+        s = ++g.zc_seq;
+    return s;
 }
 
 /* Wait for a single-call kernel's completion word (it stores `seq` at
@@ -2257,28 +2390,52 @@ static bool serve_enabled()
     return on;
 }
 
-static bool srv_launch(poporon_t *h, uint32_t last)
+/* Launch a server for the handle unless a batch of another handle on the
+ * device may still be running (then -1: the caller serves this request with
+ * one launch); 1 launched, 0 error.  Under the registry lock, so that a
+ * batch_enter either sees this server (and bumps its yield word) or is seen
+ * here. */
+static int srv_launch(poporon_t *h, uint32_t last)
 {
     GpuCtx &g = h->gpu;
     if (!g.sstream)
         HIP_OK(hipStreamCreateWithFlags(&g.sstream, hipStreamNonBlocking));
+    std::unique_lock<std::mutex> lk;
+    if (g.registered)
+        lk = std::unique_lock<std::mutex>(g_devs[g.device].mu);
+    if (g.registered)
+        for (GpuCtx *x : g_devs[g.device].ctx) {
+            if (x == &g)
+                continue;
+            if (x->batch_open)
+                return -1;
+            if (x->batch_ev_live) {
+                const hipError_t q = hipEventQuery(x->batch_ev);
+                if (q == hipErrorNotReady)
+                    return -1;
+                x->batch_ev_live = false;
+            }
+        }
+    const uint32_t yv = *reinterpret_cast<volatile uint32_t *>(g.zc + ZC_YIELD);
     const uint32_t id = g.srv_id + 1u;
     if (h->fast || h->nrsplit) {
         RsCorrParams prm = h->corr;
-        HIP_OK(rsk_serve(g.tab, &prm, g.zc_dev, last, id, SRV_IDLE_TICKS, SRV_MAX_TICKS, g.sstream));
+        HIP_OK(rsk_serve(g.tab, &prm, g.zc_dev, last, id, yv, SRV_IDLE_TICKS, SRV_MAX_TICKS, g.sstream));
     } else { /* general parameters: one wave, GZ_* payload (rs_generic.hip rsgw_serve_k) */
         RsGenParams prm = h->gen;
-        HIP_OK(rsgw_serve(g.gtab, &prm, g.zc_dev, last, id, SRV_IDLE_TICKS, SRV_MAX_TICKS, g.sstream));
+        HIP_OK(rsgw_serve(g.gtab, &prm, g.zc_dev, last, id, yv, SRV_IDLE_TICKS, SRV_MAX_TICKS, g.sstream));
     }
     g.srv_id = id;
     g.srv_on = true;
-    return true;
+    return 1;
 }
 
 /* One request through the server; the payload is in g.zc already.  A server
- * that left before it saw the request (idle limit, lifetime) has stored its
- * id to ZC_EXITED without serving it: launch a new one for it. */
-static bool srv_call(poporon_t *h, uint32_t op, uint32_t size, uint32_t mode)
+ * that left before it saw the request (idle limit, lifetime, yield) has
+ * stored its id to ZC_EXITED without serving it: launch a new one for it.
+ * 1 served, 0 error, -1 not served (another handle's batch may be running,
+ * srv_launch): the caller launches the request's kernel instead. */
+static int srv_call(poporon_t *h, uint32_t op, uint32_t size, uint32_t mode)
 {
     GpuCtx &g = h->gpu;
     volatile uint32_t *z32 = reinterpret_cast<volatile uint32_t *>(g.zc);
@@ -2287,8 +2444,11 @@ static bool srv_call(poporon_t *h, uint32_t op, uint32_t size, uint32_t mode)
     z32[ZC_FLAG / 4] = 0u; /* the server answers with the request word (never 0: op >= 1) */
     std::atomic_thread_fence(std::memory_order_release); /* the payload before the request word */
     z32[ZC_REQ / 4] = word;
-    if (!g.srv_on && !srv_launch(h, prev))
-        return false;
+    if (!g.srv_on) {
+        const int l = srv_launch(h, prev);
+        if (l <= 0)
+            return l; /* the request word stays unserved: the next server starts past it */
+    }
     const volatile uint32_t *f = z32 + ZC_FLAG / 4, *ex = z32 + ZC_EXITED / 4;
     for (uint32_t spin = 1;; ++spin) {
         if (*f == word) {
@@ -2302,8 +2462,9 @@ static bool srv_call(poporon_t *h, uint32_t op, uint32_t size, uint32_t mode)
                 return true;
             }
             g.srv_on = false;
-            if (!srv_launch(h, prev))
-                return false;
+            const int l = srv_launch(h, prev);
+            if (l <= 0)
+                return l;
             continue;
         }
         if ((spin & 4095u) == 0u) {
@@ -2381,11 +2542,11 @@ EXPORT bool poporon_encode(poporon_t *h, uint8_t *data, size_t size, uint8_t *pa
     /* (codes with fewer roots, h->nrsplit, the same way: their encq rows, P.nr) */
     if (h->fec_type == PPLN_FEC_RS && (h->fast || h->nrsplit) && size >= 1 && size <= kmax(h) && ensure_zc(g)) {
         memcpy(g.zc + ZC_DATA, data, size);
-        if (serve_enabled() && !g.timing) {
-            if (!srv_call(h, RS_SRV_ENCODE, (uint32_t)size, 0u))
-                return false;
-        } else {
-            const uint32_t seq = ++g.zc_seq;
+        const int sv = serve_enabled() && !g.timing ? srv_call(h, RS_SRV_ENCODE, (uint32_t)size, 0u) : -1;
+        if (sv == 0)
+            return false;
+        if (sv < 0) {
+            const uint32_t seq = zc_arm(g);
             KernelTimer t(g, POPORON_AMD_KERNEL_ENCODE, g.stream);
             HIP_OK(rsk_encode1_nr(g.tab, g.zc_dev + ZC_DATA, g.zc_dev + ZC_PAR, (uint32_t)size, (uint32_t)nr,
                                   reinterpret_cast<uint32_t *>(g.zc_dev + ZC_FLAG), seq, g.stream));
@@ -2399,13 +2560,13 @@ EXPORT bool poporon_encode(poporon_t *h, uint8_t *data, size_t size, uint8_t *pa
     /* general parameters: rsgw_encode_k on coherent host memory, the same way */
     if (h->fec_type == PPLN_FEC_RS && h->generic && gen_wave(h, 1, true, size) && ensure_zc(g)) {
         memcpy(g.zc + GZ_DATA, data, size);
-        if (serve_enabled() && !g.timing) {
-            if (!srv_call(h, RS_SRV_ENCODE, (uint32_t)size, 0u))
-                return false;
-        } else {
+        const int sv = serve_enabled() && !g.timing ? srv_call(h, RS_SRV_ENCODE, (uint32_t)size, 0u) : -1;
+        if (sv == 0)
+            return false;
+        if (sv < 0) {
             RsGenParams prm = h->gen;
             prm.size = (uint32_t)size;
-            const uint32_t seq = ++g.zc_seq;
+            const uint32_t seq = zc_arm(g);
             KernelTimer t(g, POPORON_AMD_KERNEL_ENCODE, g.stream);
             HIP_OK(rsgw_encode(g.gtab, &prm, g.zc_dev + GZ_DATA, size, g.zc_dev + GZ_PAR, nr, 1,
                                reinterpret_cast<uint32_t *>(g.zc_dev + ZC_FLAG), seq, g.num_cu, g.stream));
@@ -2506,11 +2667,13 @@ static bool rs_decode_one(poporon_t *h, uint8_t *data, size_t size, uint8_t *par
             prm.size = (uint32_t)size;
             prm.pad = (int32_t)(h->rs->gf->field_size - h->rs->num_roots - size);
             uint8_t *zd = g.zc_dev;
-            if (serve_enabled() && !g.timing && size == prm.size && prm.pad == (int32_t)(RS_NN - nr - size)) {
-                if (!srv_call(h, RS_SRV_DECODE, (uint32_t)size, mode))
-                    return false;
-            } else {
-                const uint32_t seq = ++g.zc_seq;
+            const int sv = serve_enabled() && !g.timing && prm.pad == (int32_t)(RS_NN - nr - size)
+                               ? srv_call(h, RS_SRV_DECODE, (uint32_t)size, mode)
+                               : -1;
+            if (sv == 0)
+                return false;
+            if (sv < 0) {
+                const uint32_t seq = zc_arm(g);
                 KernelTimer t(g, POPORON_AMD_KERNEL_SINGLE, g.stream);
                 HIP_OK(rsk_decode1(g.tab, &prm, mode, zd + ZC_DATA, zd + ZC_PAR, nullptr,
                                    reinterpret_cast<const uint32_t *>(zd + ZC_POS), zd + ZC_CNT, 4u,
@@ -2555,14 +2718,16 @@ static bool rs_decode_one(poporon_t *h, uint8_t *data, size_t size, uint8_t *par
             if (refuse) {
                 fail("external syndrome > field size: undefined in the reference, refused");
             } else {
-                if (serve_enabled() && !g.timing) {
-                    if (!srv_call(h, RS_SRV_DECODE, (uint32_t)size, ext ? 2u : pos32 ? 1u : 0u))
-                        return false;
-                } else {
+                const int sv = serve_enabled() && !g.timing
+                                   ? srv_call(h, RS_SRV_DECODE, (uint32_t)size, ext ? 2u : pos32 ? 1u : 0u)
+                                   : -1;
+                if (sv == 0)
+                    return false;
+                if (sv < 0) {
                     RsGenParams prm = h->gen;
                     prm.size = (uint32_t)size;
                     prm.pad = (int32_t)(nn - nr - size);
-                    const uint32_t seq = ++g.zc_seq;
+                    const uint32_t seq = zc_arm(g);
                     KernelTimer t(g, POPORON_AMD_KERNEL_CORRECT, g.stream);
                     HIP_OK(rsgw_decode(g.gtab, &prm, zd + GZ_DATA, size, zd + GZ_PAR, nr, 1, ext, nr, nullptr, pos32,
                                        nr, cnt, zd + GZ_OK, zd + GZ_COR, nullptr, nullptr,

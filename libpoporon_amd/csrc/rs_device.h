@@ -190,10 +190,11 @@ hipError_t rsk_decode1(const RsDevTables *tab, const RsCorrParams *prm, uint32_t
 
 /* The single-call server: one resident workgroup serving poporon_encode /
  * poporon_decode requests posted in the coherent host buffer (rs_single.hip
- * rs_serve_k); it leaves after idle_ticks (100 MHz) without a request or
- * max_ticks in all, storing `id` to ZC_EXITED. */
+ * rs_serve_k); it leaves after idle_ticks (100 MHz) without a request,
+ * max_ticks in all, or when ZC_YIELD differs from yv, storing `id` to
+ * ZC_EXITED. */
 hipError_t rsk_serve(const RsDevTables *tab, const RsCorrParams *prm, uint8_t *zc_dev, uint32_t last, uint32_t id,
-                     uint64_t idle_ticks, uint64_t max_ticks, hipStream_t stream);
+                     uint32_t yv, uint64_t idle_ticks, uint64_t max_ticks, hipStream_t stream);
 
 /* layout of the coherent host buffer of the single-call API (GpuCtx::zc) */
 #define ZC_DATA 0    /* message / data bytes (<= 223) */
@@ -212,6 +213,11 @@ hipError_t rsk_serve(const RsDevTables *tab, const RsCorrParams *prm, uint8_t *z
 #define ZC_REQ_OP(w) (((w) >> 8) & 3u)    /* RS_SRV_ENCODE / RS_SRV_DECODE */
 #define ZC_REQ_MODE(w) (((w) >> 10) & 3u) /* decode mode (rsk_decode1) */
 #define ZC_REQ_SIZE(w) ((w) & 0xFFu)      /* message bytes (1..223) */
+/* u32 beside ZC_REQ (one 8-byte poll reads both): bumped by a batch call of
+ * another handle on the device (api.cpp yield_servers); a server launched at
+ * another value leaves when no request is pending, so it does not hold a CU
+ * under that batch's persistent grids */
+#define ZC_YIELD 708
 #define ZC_EXITED 768 /* u32: the id of the last server launch that has left */
 /* general-parameter single calls (rsgw_*_k, one wave): a row of up to 255
  * symbols, up to 254 u32 slots / u16 syndromes */

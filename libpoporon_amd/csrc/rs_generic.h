@@ -48,7 +48,7 @@ hipError_t rsgw_decode(const RsGenTables *tab, const RsGenParams *prm, uint8_t *
 
 /* the general-parameter single-call server (rs_serve_k's protocol, GZ_* payload) */
 hipError_t rsgw_serve(const RsGenTables *tab, const RsGenParams *prm, uint8_t *zc_dev, uint32_t last, uint32_t id,
-                      uint64_t idle_ticks, uint64_t max_ticks, hipStream_t stream);
+                      uint32_t yv, uint64_t idle_ticks, uint64_t max_ticks, hipStream_t stream);
 hipError_t rsgw_check(const RsGenTables *tab, const RsGenParams *prm, const uint8_t *data, size_t dstride,
                       const uint8_t *parity, size_t pstride, size_t count, uint8_t *dirty, uint16_t *syn,
                       size_t syn_stride, int num_cu, hipStream_t stream);

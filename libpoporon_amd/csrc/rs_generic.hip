@@ -1145,12 +1145,13 @@ __global__ __launch_bounds__(GW_WG) void rsgw_encode_k(const RsGenTables *__rest
  * runs gw_encode_one, decode gw_decode_one in the request's mode (0 errors,
  * 1 u32 erasure slots, 2 external syndromes); then the sequence word to
  * ZC_FLAG with a system-scope release.  It leaves after idle_ticks without a
- * request, after max_ticks in all, or at RS_SRV_STOP, storing its id to
- * ZC_EXITED (api.cpp srv_call relaunches for a request it did not see).
+ * request, after max_ticks in all, at RS_SRV_STOP, or when ZC_YIELD moves
+ * off yv (another handle's batch), storing its id to ZC_EXITED (api.cpp
+ * srv_call relaunches, or launches per call, for a request it did not see).
  */
 __global__ __launch_bounds__(64) void rsgw_serve_k(const RsGenTables *__restrict__ T, RsGenParams P, uint8_t *zc,
-                                                    uint32_t last, uint32_t id, uint64_t idle_ticks,
-                                                    uint64_t max_ticks)
+                                                    uint32_t last, uint32_t id, uint32_t yv,
+                                                    uint64_t idle_ticks, uint64_t max_ticks)
 {
     __shared__ GwSmem sm;
     __shared__ uint16_t qs[GW_QS];
@@ -1161,7 +1162,7 @@ __global__ __launch_bounds__(64) void rsgw_serve_k(const RsGenTables *__restrict
     GwWave &W = sm.w[0];
     const GMod mod{P.nn, P.magic};
     const bool qf = (P.fcr + P.nroots - 1u) * P.prim + P.nn - 1u < 65536u;
-    uint32_t *req = reinterpret_cast<uint32_t *>(zc + ZC_REQ);
+    uint64_t *req = reinterpret_cast<uint64_t *>(zc + ZC_REQ); /* ZC_REQ, ZC_YIELD */
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
     uint64_t idle0 = t0;
     uint32_t staged = 0; /* message size whose rows Q[0 .. size) are in qs (0: none) */
@@ -1169,7 +1170,9 @@ __global__ __launch_bounds__(64) void rsgw_serve_k(const RsGenTables *__restrict
         if (lane == 0) {
             uint32_t r = last, op = 0;
             for (;;) {
-                r = __hip_atomic_load(req, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+                /* the request word and ZC_YIELD in one 8-byte load */
+                const uint64_t w = __hip_atomic_load(req, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+                r = (uint32_t)w;
                 if (r != last) {
                     op = ZC_REQ_OP(r);
                     cmd[2] = ZC_REQ_SIZE(r);
@@ -1177,7 +1180,7 @@ __global__ __launch_bounds__(64) void rsgw_serve_k(const RsGenTables *__restrict
                     break;
                 }
                 const uint64_t now = __builtin_amdgcn_s_memrealtime();
-                if (now - idle0 > idle_ticks || now - t0 > max_ticks)
+                if (now - idle0 > idle_ticks || now - t0 > max_ticks || (uint32_t)(w >> 32) != yv)
                     break; /* op = 0: leave */
                 __builtin_amdgcn_s_sleep(1);
             }
@@ -1358,9 +1361,10 @@ extern "C" hipError_t rsgw_check(const RsGenTables *tab, const RsGenParams *prm,
 }
 
 extern "C" hipError_t rsgw_serve(const RsGenTables *tab, const RsGenParams *prm, uint8_t *zc_dev, uint32_t last,
-                                 uint32_t id, uint64_t idle_ticks, uint64_t max_ticks, hipStream_t stream)
+                                 uint32_t id, uint32_t yv, uint64_t idle_ticks, uint64_t max_ticks,
+                                 hipStream_t stream)
 {
-    hipLaunchKernelGGL(rsgw_serve_k, dim3(1), dim3(64), 0, stream, tab, *prm, zc_dev, last, id, idle_ticks,
+    hipLaunchKernelGGL(rsgw_serve_k, dim3(1), dim3(64), 0, stream, tab, *prm, zc_dev, last, id, yv, idle_ticks,
                        max_ticks);
     return hipGetLastError();
 }

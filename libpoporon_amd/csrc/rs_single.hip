@@ -620,8 +620,11 @@ extern "C" hipError_t rsk_decode1(const RsDevTables *tab, const RsCorrParams *pr
  * The tables are filled once per launch.
  *
  * Every launch ends on its own: after idle_ticks of s_memrealtime (100 MHz)
- * without a request, after max_ticks in all, or at an RS_SRV_STOP request
- * (poporon_destroy).  It then stores its launch id to ZC_EXITED and serves
+ * without a request, after max_ticks in all, at an RS_SRV_STOP request
+ * (poporon_destroy, or a batch call on the same handle), or, with no request
+ * pending, when ZC_YIELD (read in the same 8-byte load as the request word)
+ * differs from the value it was launched with (a batch call of another
+ * handle on the device, api.cpp yield_servers).  It then stores its launch id to ZC_EXITED and serves
  * nothing more; a request the host posted meanwhile is seen unserved there
  * and the host launches a new server for it (api.cpp srv_call), on the same
  * stream, so two servers never run at once.
@@ -630,14 +633,14 @@ extern "C" hipError_t rsk_decode1(const RsDevTables *tab, const RsCorrParams *pr
 #define SRV_FULL_FENCE 0 /* 1: a system-scope release fence in every wave (measured ~1.4 us more per call) */
 #endif
 __global__ __launch_bounds__(S1_WG) void rs_serve_k(const RsDevTables *__restrict__ T, RsCorrParams P, uint8_t *zc,
-                                                    uint32_t last, uint32_t id, uint64_t idle_ticks,
-                                                    uint64_t max_ticks)
+                                                    uint32_t last, uint32_t id, uint32_t yv,
+                                                    uint64_t idle_ticks, uint64_t max_ticks)
 {
     __shared__ Dec1Smem s;
     __shared__ uint32_t cmd[4]; /* seq, op (0: leave), size, mode */
     const uint32_t t = threadIdx.x;
     fill_tabs(s.g, T, t);
-    uint32_t *req = reinterpret_cast<uint32_t *>(zc + ZC_REQ);
+    uint64_t *req = reinterpret_cast<uint64_t *>(zc + ZC_REQ); /* ZC_REQ, ZC_YIELD */
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
     uint64_t idle0 = t0;
     for (;;) {
@@ -645,7 +648,9 @@ __global__ __launch_bounds__(S1_WG) void rs_serve_k(const RsDevTables *__restric
             /* the whole request is one word: one PCIe round trip per poll */
             uint32_t r = last, op = 0;
             for (;;) {
-                r = __hip_atomic_load(req, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+                /* the request word and ZC_YIELD in one 8-byte load */
+                const uint64_t w = __hip_atomic_load(req, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+                r = (uint32_t)w;
                 if (r != last) {
                     op = ZC_REQ_OP(r); /* RS_SRV_STOP: leave */
                     cmd[2] = ZC_REQ_SIZE(r);
@@ -653,7 +658,7 @@ __global__ __launch_bounds__(S1_WG) void rs_serve_k(const RsDevTables *__restric
                     break;
                 }
                 const uint64_t now = __builtin_amdgcn_s_memrealtime();
-                if (now - idle0 > idle_ticks || now - t0 > max_ticks)
+                if (now - idle0 > idle_ticks || now - t0 > max_ticks || (uint32_t)(w >> 32) != yv)
                     break; /* op = 0: leave */
                 __builtin_amdgcn_s_sleep(1);
             }
@@ -697,9 +702,10 @@ __global__ __launch_bounds__(S1_WG) void rs_serve_k(const RsDevTables *__restric
 }
 
 extern "C" hipError_t rsk_serve(const RsDevTables *tab, const RsCorrParams *prm, uint8_t *zc_dev, uint32_t last,
-                                uint32_t id, uint64_t idle_ticks, uint64_t max_ticks, hipStream_t stream)
+                                uint32_t id, uint32_t yv, uint64_t idle_ticks, uint64_t max_ticks,
+                                hipStream_t stream)
 {
-    hipLaunchKernelGGL(rs_serve_k, dim3(1), dim3(S1_WG), 0, stream, tab, *prm, zc_dev, last, id, idle_ticks,
+    hipLaunchKernelGGL(rs_serve_k, dim3(1), dim3(S1_WG), 0, stream, tab, *prm, zc_dev, last, id, yv, idle_ticks,
                        max_ticks);
     return hipGetLastError();
 }

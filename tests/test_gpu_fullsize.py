@@ -372,3 +372,100 @@ def test_c_dropin_programs():
     r = subprocess.run([os.path.join(d, "test_rs_api")], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stderr + r.stdout
     assert "all checks passed" in r.stdout
+
+
+# ---------------------------------------------------------------------------
+# one handle's batches beside another handle's single calls
+# ---------------------------------------------------------------------------
+def test_batch_beside_other_handle_single_calls(oracle_default, torch_cuda):
+    """Handle B runs poporon_decode in a C loop on a host thread (the
+    reference's calling pattern, SURVEY §8b: distinct handles are
+    independent) while handle A encodes and decodes 2^20 codewords on the
+    device.  A batch call makes B's resident server leave (ZC_YIELD) and keeps
+    it from relaunching until the batch has run (api.cpp yield_servers /
+    srv_launch), so A's persistent grids never wait for a CU B's server
+    holds: A's results are bit-exact and A's GPU time stays within 1.2x of its
+    time with B idle; every one of B's results equals the oracle's."""
+    import threading
+
+    torch = torch_cuda
+    lib = P.load_library()
+    A, B = P.Poporon.default(), P.Poporon.default()
+    n = 1 << 20
+    s = _stream(torch)
+    rows = _synth(torch, n, seed=SEED + 40)
+    b = rows.data_ptr()
+    A.encode_batch_device(b, N, b + K, N, K, n, s)
+    torch.cuda.synchronize()
+    clean = rows.clone()
+    clean_sum = _checksum(torch, rows)
+    pos, mag = _errors(torch, n, 16, N, SEED + 41)
+    ok = torch.zeros(n, dtype=torch.uint8, device="cuda")
+    cor = torch.zeros(n, dtype=torch.uint8, device="cuda")
+
+    # B's codewords: 8 errors each, expected results from the oracle
+    rng = np.random.default_rng(77)
+    nb = 1500
+    bd = rng.integers(0, 256, (nb, K), dtype=np.uint8)
+    bp = oracle_default.encode_batch(bd)
+    bcw = np.concatenate([bd, bp], 1)
+    for c in range(nb):
+        p = rng.permutation(N)[:8]
+        bcw[c, p] ^= rng.integers(1, 256, 8, dtype=np.uint8)
+    wok, wcor, wd, wp = oracle_default.decode_batch(bcw[:, :K], bcw[:, K:])
+    stop = threading.Event()
+    b_calls, b_bad = [0], [0]
+
+    def b_loop():
+        while not stop.is_set():
+            d, p = bcw[:, :K].copy(), bcw[:, K:].copy()
+            t, gok, gcor = T.time_decode(lib, B.h, d, p)
+            assert t >= 0
+            b_calls[0] += nb
+            b_bad[0] += int((gok != wok).sum() + (gcor != wcor).sum() + (d != wd).any(1).sum() + (p != wp).any(1).sum())
+
+    enc = clean.clone()  # A's encode input: the clean messages, parity rewritten in place
+    eb = enc.data_ptr()
+
+    def run_a():
+        """A's encode + decode on the GPU clock; the stream is kept busy while
+        the host enqueues, so host-side delays are not counted"""
+        rows.copy_(clean)
+        T.channel_xor(pos.data_ptr(), mag.data_ptr(), 16, b, N, n, s)
+        enc[:, K:] = 0
+        torch.cuda.synchronize()
+        torch.cuda._sleep(2_000_000)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        A.encode_batch_device(eb, N, eb + K, N, K, n, s)
+        A.decode_batch_device(b, N, b + K, N, K, n, ok.data_ptr(), cor.data_ptr(), stream=s)
+        e1.record()
+        torch.cuda.synchronize()
+        return e0.elapsed_time(e1)
+
+    def check_a():
+        assert torch.equal(enc, clean)
+        assert bool((ok == 1).all()) and bool((cor == 16).all())
+        assert torch.equal(rows, clean)
+
+    alone = [run_a() for _ in range(6)][1:]
+    check_a()
+    # B's server is resident before A's batches start
+    assert B.decode(bcw[0, :K].copy(), bcw[0, K:].copy())[0] == bool(wok[0])
+    th = threading.Thread(target=b_loop)
+    th.start()
+    try:
+        import time
+        time.sleep(0.05)
+        beside = [run_a() for _ in range(6)][1:]
+        check_a()
+    finally:
+        stop.set()
+        th.join()
+    assert b_calls[0] > 0 and b_bad[0] == 0, (b_calls[0], b_bad[0])
+    ma, mb = float(np.median(alone)), float(np.median(beside))
+    print(f"A alone {ma:.3f} ms, beside B's single calls {mb:.3f} ms, B calls {b_calls[0]}")
+    assert mb <= 1.2 * ma, (alone, beside)
+    sample = clean[::4096].cpu().numpy()
+    assert (oracle_default.encode_batch(sample[:, :K]) == sample[:, K:]).all()
+    assert _checksum(torch, rows) == clean_sum

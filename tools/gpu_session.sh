@@ -26,6 +26,13 @@ for step in "$@"; do
     tests) run tests 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread ;;
     tests_all) run tests_all 900 python -m pytest tests -m gpu -q ;;
     bench) run bench 600 python bench.py ;;
+    beside) # the cross-handle batch / single-call test on each build in build/*.so, then the tree's
+        for so in build/*.so; do
+            POPORON_AMD_LIB=$so run "beside_$(basename $so .so)" 300 python -u -m pytest tests/test_gpu_fullsize.py \
+                -k beside -v -s --timeout 250 --timeout-method thread
+        done
+        run beside_tree 300 python -u -m pytest tests/test_gpu_fullsize.py -k beside -v -s --timeout 250 \
+            --timeout-method thread ;;
     lat) run lat 200 python tools/lat_single.py 2000
          POPORON_AMD_SERVE=0 run lat_noserve 200 python tools/lat_single.py 2000 ;;
     bsz) run bsz 700 bash tools/batch_sizes.sh ;;
