@@ -633,7 +633,7 @@ __global__ __launch_bounds__(F2WG, F2_WAVES) void rs_forney_k(const RsDevTables 
  * left to the errata kernels (RS_ST_PEND) or goes to the list (rs_correct_k
  * in record mode).  Output: the 64-byte record of rs_apply_k<32> (slots,
  * magnitudes).  The round-3 kernel that ran the locator, Omega and Forney
- * here: tools/experiments/rs_era_forney_k.hip.txt.
+ * here: profiles/experiments/rs_era_forney_k.hip.txt.
  */
 /*
  * The magnitudes are solved directly.  With 32 erasures the 32 syndromes determine them: S_i =

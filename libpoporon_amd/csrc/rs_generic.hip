@@ -435,23 +435,36 @@ __global__ __launch_bounds__(G_WG_MAX) void rsg_check_k(const RsGenTables *__res
 #define GW_AL2 1536 /* al2[x] = alpha^(x mod nn) for x < 2 nn, 0 from there on */
 #define GW_QS 16384 /* max size * nr with size + nr <= 255: 127 * 128 (u16: 32 KB) */
 
-struct GwWave {
-    uint8_t cw[256];    /* the received row [data | parity], raw bytes */
-    uint16_t lr[256];   /* log of each masked byte (GW_Z: zero) */
-    uint8_t S[256];     /* syndromes, log form (nn: zero) */
-    uint16_t sz[256];   /* the same, GW_Z for zero */
-    uint16_t lamz[256]; /* locator, log form, GW_Z for zero */
-    uint16_t omz[256];  /* Omega, log form, GW_Z for zero */
-    uint16_t lgm[256];  /* per root: log of its magnitude (0xffff: zero) ... */
-    uint16_t lx[256];   /* ... and nn - 1 - its location (the re-syndrome check's factor) */
-    uint8_t roots[256], locs[256], mag[256];
-    uint32_t acc[256];  /* syndrome partial sums / erasure slots / apply deltas */
+/* one codeword's LDS state; N = 4 x the lanes per codeword (indices i on
+ * lane i % GL, register slot i / GL) */
+template <int N>
+struct GwRowT {
+    uint8_t cw[N];    /* the received row [data | parity], raw bytes */
+    uint16_t lr[N];   /* log of each masked byte (GW_Z: zero) */
+    uint8_t S[N];     /* syndromes, log form (nn: zero) */
+    uint16_t sz[N];   /* the same, GW_Z for zero */
+    uint16_t lamz[N]; /* locator, log form, GW_Z for zero */
+    uint16_t omz[N];  /* Omega, log form, GW_Z for zero */
+    uint16_t lgm[N];  /* per root: log of its magnitude (0xffff: zero) ... */
+    uint16_t lx[N];   /* ... and nn - 1 - its location (the re-syndrome check's factor) */
+    uint8_t roots[N], locs[N], mag[N];
+    uint32_t acc[N];  /* syndrome partial sums / erasure slots / apply deltas */
 };
+typedef GwRowT<256> GwWave;
 
 struct GwSmem {
     uint8_t alog[256], log[256];
     uint8_t al2[GW_AL2];
     GwWave w[GW_WG / 64];
+};
+
+/* GL lanes per codeword: 64 / GL codewords per wave (codes of up to 4 GL - 1
+ * symbols) */
+template <int GL>
+struct GwSmemG {
+    uint8_t alog[256], log[256];
+    uint8_t al2[GW_AL2];
+    GwRowT<4 * GL> w[GW_WG / GL];
 };
 
 /* lane order within a wave: LDS writes by some lanes, then reads by others */
@@ -506,6 +519,72 @@ __device__ __forceinline__ void gw_shift(const uint32_t (&v)[4], uint32_t (&out)
     }
 }
 
+/* The GL lanes of a wave that share one codeword (GL = 64: the whole wave;
+ * 32: a half; 16: a DPP row): the index within the group, the group's bits of
+ * a ballot, the XOR over the group and the shift by one index (slot carry
+ * from the group's last lane).  Groups run the same code; their branches
+ * diverge per codeword. */
+template <int GL>
+struct GwGrp {
+    uint32_t gl; /* lane within the group */
+    uint32_t gb; /* the group's first lane in the wave */
+    __device__ __forceinline__ explicit GwGrp(uint32_t lane) : gl(lane % GL), gb(lane - lane % GL) {}
+    __device__ __forceinline__ uint64_t ballot(bool p) const
+    {
+        const uint64_t m = __ballot(p);
+        if constexpr (GL == 64)
+            return m;
+        else
+            return (m >> gb) & ((1ull << GL) - 1ull);
+    }
+    __device__ __forceinline__ bool any(bool p) const { return ballot(p) != 0ull; }
+    __device__ __forceinline__ uint64_t below() const { return (1ull << gl) - 1ull; }
+    __device__ __forceinline__ uint32_t xr(uint32_t v) const
+    {
+        if constexpr (GL == 64)
+            return gw_xor(v);
+        if constexpr (GL == 32) {
+            const auto b = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+            v = b[0] ^ b[1];
+        }
+        v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x128, 0xf, 0xf, false); /* row_ror:8 */
+        v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x124, 0xf, 0xf, false); /* row_ror:4 */
+        v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xf, 0xf, false);  /* quad_perm [2,3,0,1] */
+        v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xf, 0xf, false);  /* quad_perm [1,0,3,2] */
+        return v;
+    }
+    /* out[i] = v[i - 1] over the four slots (index i = gl + GL q), out[0] = first */
+    __device__ __forceinline__ void shift(const uint32_t (&v)[4], uint32_t (&out)[4], uint32_t first,
+                                          uint32_t nq) const
+    {
+        if constexpr (GL == 64) {
+            gw_shift(v, out, gl, first, nq);
+        } else if constexpr (GL == 32) {
+            uint32_t carry = first;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                if ((uint32_t)q < nq) {
+                    const uint32_t t0 = (uint32_t)__builtin_amdgcn_readlane((int)v[q], 31);
+                    const uint32_t t1 = (uint32_t)__builtin_amdgcn_readlane((int)v[q], 63);
+                    const uint32_t u = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v[q], 0x138, 0xf, 0xf, true);
+                    out[q] = gl ? u : carry; /* wave_shr:1; each half's lane 0 takes the carry */
+                    carry = gb ? t1 : t0;
+                }
+            }
+        } else {
+            uint32_t carry = first;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                if ((uint32_t)q < nq) {
+                    const uint32_t u = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v[q], 0x121, 0xf, 0xf, false);
+                    out[q] = gl ? u : carry; /* row_ror:1: lane 0 sees lane 15, the next slot's carry */
+                    carry = u;
+                }
+            }
+        }
+    }
+};
+
 /* the tables: one global load per thread and table, al2 from the LDS copy
  * (its six entries per thread loaded from global one after another had cost
  * a few us per launch) */
@@ -515,7 +594,8 @@ __device__ __forceinline__ void gw_fill_al2(uint8_t *al2, const uint8_t *alog_ld
         al2[x] = x < nn ? alog_lds[x] : (x < 2u * nn ? alog_lds[x - nn] : (uint8_t)0);
 }
 
-__device__ __forceinline__ void gw_tables(GwSmem &sm, const RsGenTables *__restrict__ T, uint32_t nn)
+template <typename SM>
+__device__ __forceinline__ void gw_tables(SM &sm, const RsGenTables *__restrict__ T, uint32_t nn)
 {
     for (uint32_t t = threadIdx.x; t < 256u; t += blockDim.x) {
         sm.alog[t] = T->alog[t];
@@ -531,56 +611,58 @@ __device__ __forceinline__ void gw_tables(GwSmem &sm, const RsGenTables *__restr
  * mod nn) and S_i = sum_b r_b alpha^(s_i (total - 1 - b)): independent terms,
  * G = 64 / nr lanes per root for short root counts (partial sums XORed in
  * LDS).  Else the reference's Horner, one root per lane. */
-__device__ bool gw_syndromes(const GwSmem &sm, GwWave &W, const RsGenParams &P, const GMod &mod, uint32_t lane,
-                             bool qf)
+template <int GL, typename SM, typename WT>
+__device__ bool gw_syndromes(const SM &sm, WT &W, const RsGenParams &P, const GMod &mod, const GwGrp<GL> &G, bool qf)
 {
+    constexpr uint32_t GLU = GL;
+    const uint32_t lane = G.gl;
     const uint32_t nr = P.nroots, nn = P.nn, A0 = P.nn, total = P.size + nr;
     const uint8_t *al2 = sm.al2, *lg = sm.log, *alog = sm.alog;
     uint32_t sv[4] = {0, 0, 0, 0};
     if (qf) {
-        const uint32_t G = nr <= 32u ? 64u / nr : 1u;
-        const uint32_t U = nr * G;
-        if (G > 1u) {
+        const uint32_t Gr = nr <= GLU / 2u ? GLU / nr : 1u;
+        const uint32_t U = nr * Gr;
+        if (Gr > 1u) {
             if (lane < nr)
                 W.acc[lane] = 0;
             gw_sync();
         }
         /* G > 1: one unit per lane (q = 0); G = 1: units lane + 64 q, all over
          * every byte -- one broadcast read of the byte's log for all of them */
-        const uint32_t g = G > 1u ? lane / nr : 0u;
-        const uint32_t nq = (U + 63u) / 64u; /* register slots in use (uniform) */
+        const uint32_t g = Gr > 1u ? lane / nr : 0u;
+        const uint32_t nq = (U + GLU - 1u) / GLU; /* register slots in use (uniform) */
         uint32_t e[4], sg[4];
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-            const uint32_t u = lane + 64u * q;
-            const uint32_t i = G > 1u ? lane % nr : u;
+            const uint32_t u = lane + GLU * q;
+            const uint32_t i = Gr > 1u ? lane % nr : u;
             const uint32_t sx = mod((P.fcr + i) * P.prim);
-            sg[q] = mod(sx * G);
+            sg[q] = mod(sx * Gr);
             e[q] = g < total ? mod(sx * (total - 1u - g)) : 0u;
         }
-        if (lane + 64u * 0u < U) {
+        if (lane < U) {
 #pragma unroll 4
-            for (uint32_t b = g; b < total; b += G) {
+            for (uint32_t b = g; b < total; b += Gr) {
                 const uint32_t l = W.lr[b];
 #pragma unroll
                 for (int q = 0; q < 4; ++q) {
-                    if ((uint32_t)q < nq && lane + 64u * q < U) { /* q > 0 only for G = 1: the same b for every q */
+                    if ((uint32_t)q < nq && lane + GLU * q < U) { /* q > 0 only for G = 1: the same b for every q */
                         sv[q] ^= al2[l + e[q]];
                         e[q] = e[q] >= sg[q] ? e[q] - sg[q] : e[q] + nn - sg[q];
                     }
                 }
             }
         }
-        if (G > 1u && lane < U)
+        if (Gr > 1u && lane < U)
             atomicXor(&W.acc[lane % nr], sv[0]);
-        if (G > 1u) {
+        if (Gr > 1u) {
             gw_sync();
             sv[0] = lane < nr ? W.acc[lane] : 0u;
         }
     } else {
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-            const uint32_t i = lane + 64u * q;
+            const uint32_t i = lane + GLU * q;
             if (i < nr) {
                 const uint32_t step = P.fcr * P.prim + i * P.prim; /* int arithmetic, truncated inside gf_mod */
                 uint32_t v = (uint32_t)W.cw[0] & A0;
@@ -595,7 +677,7 @@ __device__ bool gw_syndromes(const GwSmem &sm, GwWave &W, const RsGenParams &P, 
     bool nz = false;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-        const uint32_t i = lane + 64u * q;
+        const uint32_t i = lane + GLU * q;
         if (i < nr) {
             const uint32_t l = lg[sv[q]];
             W.S[i] = (uint8_t)l;
@@ -604,38 +686,40 @@ __device__ bool gw_syndromes(const GwSmem &sm, GwWave &W, const RsGenParams &P, 
         }
     }
     gw_sync();
-    return __ballot(nz) != 0ull;
+    return G.any(nz);
 }
 
 /* src/decode.c:17-230 for the row in W (syndromes in W.S / W.sz): erasure
  * locator, BM, degree, Chien, Omega, Forney, re-syndrome check, apply
  * (in place in data / parity from W.cw).  Same results as g_correct. */
-template <typename PosT>
-__device__ bool gw_correct(const GwSmem &sm, GwWave &W, const RsGenParams &P, const GMod &mod, uint32_t lane,
+template <typename PosT, int GL, typename SM, typename WT>
+__device__ bool gw_correct(const SM &sm, WT &W, const RsGenParams &P, const GMod &mod, const GwGrp<GL> &G,
                            uint8_t *data, uint8_t *parity, uint32_t ne, const PosT *pos, bool eras_apply,
                            uint32_t &corrected)
 {
+    constexpr uint32_t GLU = GL;
+    const uint32_t lane = G.gl;
     const uint32_t nr = P.nroots, nn = P.nn, A0 = P.nn, size = P.size;
     const int32_t pad = P.pad;
     const uint8_t *alog = sm.alog, *lg = sm.log, *al2 = sm.al2;
-    const uint32_t nq = (nr + 64u) / 64u; /* register slots holding indices 0 .. nr (uniform) */
+    const uint32_t nq = (nr + GLU) / GLU; /* register slots holding indices 0 .. nr (uniform) */
     uint32_t lam[4], B[4], Bm[4];
 #pragma unroll
     for (int q = 0; q < 4; ++q)
-        lam[q] = (lane + 64u * q) == 0u ? 1u : 0u;
+        lam[q] = (lane + GLU * q) == 0u ? 1u : 0u;
 
     /* erasure locator prod (1 + X_l x), src/decode.c:31-47 */
     if (ne > 0u) {
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-            const uint32_t i = lane + 64u * q;
+            const uint32_t i = lane + GLU * q;
             if (i < ne)
                 W.acc[i] = (uint32_t)pos[i];
         }
         gw_sync();
         for (uint32_t e = 0; e < ne; ++e) {
             const uint32_t xl = mod(P.prim * (A0 - 1u - (W.acc[e] + (uint32_t)pad)));
-            gw_shift(lam, Bm, lane, 0u, nq);
+            G.shift(lam, Bm, 0u, nq);
 #pragma unroll
             for (int q = 0; q < 4; ++q)
                 if ((uint32_t)q < nq && Bm[q] != 0u)
@@ -652,23 +736,23 @@ __device__ bool gw_correct(const GwSmem &sm, GwWave &W, const RsGenParams &P, co
         uint32_t part = 0;
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-            const uint32_t i = lane + 64u * q;
+            const uint32_t i = lane + GLU * q;
             if ((uint32_t)q < nq && i < r && lam[q] != 0u) {
                 const uint32_t sv = W.S[r - i - 1u];
                 if (sv != A0)
                     part ^= al2[lg[lam[q]] + sv];
             }
         }
-        const uint32_t disc = lg[gw_xor(part)];
+        const uint32_t disc = lg[G.xr(part)];
         if (disc == A0) {
-            gw_shift(B, Bm, lane, A0, nq);
+            G.shift(B, Bm, A0, nq);
 #pragma unroll
             for (int q = 0; q < 4; ++q)
                 B[q] = Bm[q];
             continue;
         }
         const bool lengthen = 2u * L <= r + ne - 1u;
-        gw_shift(B, Bm, lane, A0, nq);
+        G.shift(B, Bm, A0, nq);
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
             if ((uint32_t)q >= nq)
@@ -691,14 +775,14 @@ __device__ bool gw_correct(const GwSmem &sm, GwWave &W, const RsGenParams &P, co
     uint32_t deg = 0;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-        const uint32_t i = lane + 64u * q;
+        const uint32_t i = lane + GLU * q;
         const uint32_t l = lg[lam[q]];
         const bool valid = (uint32_t)q < nq && i <= nr;
         if (valid)
             W.lamz[i] = l == A0 ? GW_Z : l;
-        const uint64_t m = __ballot(valid && l != A0);
+        const uint64_t m = G.ballot(valid && l != A0);
         if (m)
-            deg = 64u * q + 63u - (uint32_t)__clzll((long long)m);
+            deg = GLU * q + 63u - (uint32_t)__clzll((long long)m);
     }
     if (deg == 0u)
         return false;
@@ -710,12 +794,12 @@ __device__ bool gw_correct(const GwSmem &sm, GwWave &W, const RsGenParams &P, co
         uint32_t acc[4], pm[4], tt[4];
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-            const uint32_t pt = lane + 1u + 64u * q;
+            const uint32_t pt = lane + 1u + GLU * q;
             pm[q] = pt >= nn ? pt - nn : pt;
             acc[q] = 1;
             tt[q] = 0;
         }
-        const uint32_t np = (nn + 63u) / 64u; /* slots holding the points 1 .. nn (uniform) */
+        const uint32_t np = (nn + GLU - 1u) / GLU; /* slots holding the points 1 .. nn (uniform) */
 #pragma unroll 4
         for (uint32_t j = 1; j <= deg; ++j) {
             const uint32_t lz = W.lamz[j];
@@ -730,12 +814,12 @@ __device__ bool gw_correct(const GwSmem &sm, GwWave &W, const RsGenParams &P, co
         }
         uint32_t base = 0;
         bool padbad = false;
-        const uint64_t below = (1ull << lane) - 1ull;
+        const uint64_t below = G.below();
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-            const uint32_t pt = lane + 1u + 64u * q;
+            const uint32_t pt = lane + 1u + GLU * q;
             const bool root = pt <= nn && acc[q] == 0u;
-            const uint64_t m = __ballot(root);
+            const uint64_t m = G.ballot(root);
             const uint32_t rank = base + (uint32_t)__popcll(m & below);
             if (root && rank < deg) {
                 const uint32_t k = mod(pt * P.iprim - 1u);
@@ -745,7 +829,7 @@ __device__ bool gw_correct(const GwSmem &sm, GwWave &W, const RsGenParams &P, co
             }
             base += (uint32_t)__popcll(m);
         }
-        if (__ballot(padbad) != 0ull || base < deg)
+        if (G.any(padbad) || base < deg)
             return false;
     }
     gw_sync();
@@ -753,7 +837,7 @@ __device__ bool gw_correct(const GwSmem &sm, GwWave &W, const RsGenParams &P, co
     /* Omega = S Lambda mod x^deg, log form, src/decode.c:147-158 */
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-        const uint32_t i = lane + 64u * q;
+        const uint32_t i = lane + GLU * q;
         if (i < deg) {
             uint32_t acc = 0;
 #pragma unroll 4
@@ -769,7 +853,7 @@ __device__ bool gw_correct(const GwSmem &sm, GwWave &W, const RsGenParams &P, co
     uint32_t fixed = 0;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-        const uint32_t jj = lane + 64u * q;
+        const uint32_t jj = lane + GLU * q;
         uint32_t num = 0;
         if (jj < deg) {
             const uint32_t rt = W.roots[jj];
@@ -794,7 +878,7 @@ __device__ bool gw_correct(const GwSmem &sm, GwWave &W, const RsGenParams &P, co
             W.lgm[jj] = mg ? (uint32_t)lg[mg] : 0xffffu;
             W.lx[jj] = A0 - (uint32_t)W.locs[jj] - 1u;
         }
-        fixed += (uint32_t)__popcll(__ballot(jj < deg && num != 0u));
+        fixed += (uint32_t)__popcll(G.ballot(jj < deg && num != 0u));
     }
     corrected = fixed;
     gw_sync();
@@ -804,7 +888,7 @@ __device__ bool gw_correct(const GwSmem &sm, GwWave &W, const RsGenParams &P, co
         bool bad = false;
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-            const uint32_t i = lane + 64u * q;
+            const uint32_t i = lane + GLU * q;
             if (i < nr) {
                 uint32_t acc = 0;
                 const uint32_t fi = (P.fcr + i) * P.prim;
@@ -818,7 +902,7 @@ __device__ bool gw_correct(const GwSmem &sm, GwWave &W, const RsGenParams &P, co
                 bad |= acc != alog[W.S[i]];
             }
         }
-        if (__ballot(bad) != 0ull)
+        if (G.any(bad))
             return false;
     }
 
@@ -831,7 +915,7 @@ __device__ bool gw_correct(const GwSmem &sm, GwWave &W, const RsGenParams &P, co
         gw_sync();
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-            const uint32_t jj = lane + 64u * q;
+            const uint32_t jj = lane + GLU * q;
             if (jj < deg) {
                 const uint32_t p = (uint32_t)pos[jj], mg = W.mag[jj];
                 if (mg != 0u && p < total)
@@ -841,7 +925,7 @@ __device__ bool gw_correct(const GwSmem &sm, GwWave &W, const RsGenParams &P, co
         gw_sync();
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-            const uint32_t b = lane + 64u * q;
+            const uint32_t b = lane + GLU * q;
             if (b < total) {
                 const uint32_t dl = (W.acc[b >> 2] >> (8u * (b & 3u))) & 0xffu;
                 if (dl != 0u) {
@@ -860,15 +944,15 @@ __device__ bool gw_correct(const GwSmem &sm, GwWave &W, const RsGenParams &P, co
     uint32_t first_bad = deg;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-        const uint32_t jj = lane + 64u * q;
-        const int32_t p = (int32_t)W.locs[jj < 256u ? jj : 0u] - pad;
-        const uint64_t m = __ballot(jj < deg && !(p >= 0 && p < (int32_t)total));
+        const uint32_t jj = lane + GLU * q;
+        const int32_t p = (int32_t)W.locs[jj < 4u * GLU ? jj : 0u] - pad;
+        const uint64_t m = G.ballot(jj < deg && !(p >= 0 && p < (int32_t)total));
         if (m != 0ull && first_bad == deg)
-            first_bad = 64u * q + (uint32_t)__builtin_ctzll(m);
+            first_bad = GLU * q + (uint32_t)__builtin_ctzll(m);
     }
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-        const uint32_t jj = lane + 64u * q;
+        const uint32_t jj = lane + GLU * q;
         if (jj < first_bad) {
             const uint32_t p = (uint32_t)((int32_t)W.locs[jj] - pad), mg = W.mag[jj];
             if (mg != 0u) {
@@ -886,15 +970,17 @@ __device__ bool gw_correct(const GwSmem &sm, GwWave &W, const RsGenParams &P, co
 /* One codeword on one wave, branch logic of src/decode.c:431-487: x (the
  * row's external log-form syndromes) or pos / ne (its erasure slots and
  * count) or neither; ok / corrected_num to okp / corp (corp may be NULL) */
-template <typename PosT>
-__device__ void gw_decode_one(const GwSmem &sm, GwWave &W, const RsGenParams &P, const GMod &mod, uint32_t lane,
+template <typename PosT, int GL, typename SM, typename WT>
+__device__ void gw_decode_one(const SM &sm, WT &W, const RsGenParams &P, const GMod &mod, const GwGrp<GL> &G,
                               bool qf, uint8_t *d, uint8_t *par, const uint16_t *x, const PosT *pos, uint32_t ne,
                               uint8_t *okp, uint8_t *corp)
 {
+    constexpr uint32_t GLU = GL;
+    const uint32_t lane = G.gl;
     const uint32_t nr = P.nroots, A0 = P.nn, size = P.size, total = size + nr;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-        const uint32_t b = lane + 64u * q;
+        const uint32_t b = lane + GLU * q;
         const uint32_t v = b < size ? d[b] : (b < total ? par[b - size] : 0u);
         const uint32_t m = v & A0;
         W.cw[b] = (uint8_t)v;
@@ -906,7 +992,7 @@ __device__ void gw_decode_one(const GwSmem &sm, GwWave &W, const RsGenParams &P,
         bool bad = false, any = false;
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-            const uint32_t i = lane + 64u * q;
+            const uint32_t i = lane + GLU * q;
             if (i < nr) {
                 const uint32_t v = x[i];
                 bad |= v > A0;
@@ -915,18 +1001,18 @@ __device__ void gw_decode_one(const GwSmem &sm, GwWave &W, const RsGenParams &P,
                 W.sz[i] = v == A0 ? GW_Z : (v & 0xffu);
             }
         }
-        bad = __ballot(bad) != 0ull;
-        any = __ballot(any) != 0ull;
+        bad = G.any(bad);
+        any = G.any(any);
         gw_sync();
         good = !bad &&
-               (!any || gw_correct<PosT>(sm, W, P, mod, lane, d, par, 0u, (const PosT *)nullptr, false, fixed));
+               (!any || gw_correct<PosT>(sm, W, P, mod, G, d, par, 0u, (const PosT *)nullptr, false, fixed));
     } else {
         gw_sync();
-        const bool dirty = gw_syndromes(sm, W, P, mod, lane, qf);
+        const bool dirty = gw_syndromes(sm, W, P, mod, G, qf);
         if (pos)
-            good = !dirty || (ne <= nr && gw_correct<PosT>(sm, W, P, mod, lane, d, par, ne, pos, true, fixed));
+            good = !dirty || (ne <= nr && gw_correct<PosT>(sm, W, P, mod, G, d, par, ne, pos, true, fixed));
         else
-            good = !dirty || gw_correct<PosT>(sm, W, P, mod, lane, d, par, 0u, (const PosT *)nullptr, false, fixed);
+            good = !dirty || gw_correct<PosT>(sm, W, P, mod, G, d, par, 0u, (const PosT *)nullptr, false, fixed);
     }
     if (lane == 0u) {
         *okp = good ? 1 : 0;
@@ -936,9 +1022,10 @@ __device__ void gw_decode_one(const GwSmem &sm, GwWave &W, const RsGenParams &P,
     gw_sync();
 }
 
-/* Full decode, one codeword per wave (rsg_decode_k's modes: ext / erasure
- * slots / errors; list mode) */
-template <typename PosT>
+/* Full decode, one codeword per GL lanes (rsg_decode_k's modes: ext /
+ * erasure slots / errors; list mode): GL = 64 one codeword per wave, 32 / 16
+ * two / four per wave for codes of up to 127 / 63 symbols */
+template <typename PosT, int GL>
 __global__ __launch_bounds__(GW_WG, 4) void rsgw_decode_k(const RsGenTables *__restrict__ T, RsGenParams P,
                                                            uint8_t *data, size_t dstride, uint8_t *parity,
                                                            size_t pstride, size_t count,
@@ -950,21 +1037,24 @@ __global__ __launch_bounds__(GW_WG, 4) void rsgw_decode_k(const RsGenTables *__r
                                                            const uint32_t *__restrict__ list_n, uint32_t *flag,
                                                            uint32_t seq)
 {
+    constexpr uint32_t CPB = GW_WG / GL; /* codewords per workgroup pass */
     const size_t n = list ? (size_t)*list_n : count;
-    if ((size_t)blockIdx.x * (GW_WG / 64) >= n)
+    if ((size_t)blockIdx.x * CPB >= n)
         return;
-    __shared__ GwSmem sm;
-    const uint32_t t = threadIdx.x, lane = t & 63u, wave = t >> 6;
+    __shared__ GwSmemG<GL> sm;
+    const uint32_t t = threadIdx.x;
+    const GwGrp<GL> G(t & 63u);
+    const uint32_t slot = t / GL;
     gw_tables(sm, T, P.nn);
     __syncthreads();
-    GwWave &W = sm.w[wave];
+    auto &W = sm.w[slot];
     const GMod mod{P.nn, P.magic};
     const bool qf = (P.fcr + P.nroots - 1u) * P.prim + P.nn - 1u < 65536u;
-    for (size_t e = (size_t)blockIdx.x * (GW_WG / 64) + wave; e < n; e += (size_t)gridDim.x * (GW_WG / 64)) {
+    for (size_t e = (size_t)blockIdx.x * CPB + slot; e < n; e += (size_t)gridDim.x * CPB) {
         const size_t cw = list ? (size_t)list[e] : e;
-        gw_decode_one<PosT>(sm, W, P, mod, lane, qf, data + cw * dstride, parity + cw * pstride,
-                            ext ? ext + cw * ext_stride : nullptr, pos ? pos + cw * pos_stride : nullptr,
-                            pos ? (uint32_t)cntv[cw] : 0u, ok + cw, corrected ? corrected + cw : nullptr);
+        gw_decode_one<PosT, GL>(sm, W, P, mod, G, qf, data + cw * dstride, parity + cw * pstride,
+                                ext ? ext + cw * ext_stride : nullptr, pos ? pos + cw * pos_stride : nullptr,
+                                pos ? (uint32_t)cntv[cw] : 0u, ok + cw, corrected ? corrected + cw : nullptr);
     }
     gw_done(flag, seq);
 }
@@ -997,7 +1087,7 @@ __global__ __launch_bounds__(GW_WG) void rsgw_check_k(const RsGenTables *__restr
             W.lr[b] = m ? (uint32_t)sm.log[m] : GW_Z;
         }
         gw_sync();
-        const bool nz = gw_syndromes(sm, W, P, mod, lane, qf);
+        const bool nz = gw_syndromes(sm, W, P, mod, GwGrp<64>(lane), qf);
         if (dirty && lane == 0u)
             dirty[e] = nz ? 1 : 0;
         if (syn) /* log form, the reference's uint16 array (src/decode.c:409-412) */
@@ -1203,7 +1293,7 @@ __global__ __launch_bounds__(64) void rsgw_serve_k(const RsGenTables *__restrict
             }
             gw_encode_one(sm.al2, sm.log, W.lr, qs, Q, lane, size > P.nroots, zc + GZ_DATA, zc + GZ_PAR);
         } else {
-            gw_decode_one<uint32_t>(sm, W, Q, mod, lane, qf, zc + GZ_DATA, zc + GZ_PAR,
+            gw_decode_one<uint32_t, 64>(sm, W, Q, mod, GwGrp<64>(lane), qf, zc + GZ_DATA, zc + GZ_PAR,
                                     mode == 2u ? reinterpret_cast<const uint16_t *>(zc + GZ_EXT) : nullptr,
                                     mode == 1u ? reinterpret_cast<const uint32_t *>(zc + GZ_POS) : nullptr,
                                     mode == 1u ? (uint32_t)zc[GZ_CNT] : 0u, zc + GZ_OK, zc + GZ_COR);
@@ -1330,6 +1420,35 @@ extern "C" hipError_t rsgw_encode(const RsGenTables *tab, const RsGenParams *prm
     return hipGetLastError();
 }
 
+/* lanes per codeword of a decode batch: four codewords per wave for codes of
+ * up to 63 symbols, two up to 127, from GW_GROUP_MIN codewords on (single
+ * calls and small batches keep the whole wave: the shortest chain per
+ * codeword) */
+#ifndef GW_GROUP_MIN
+#define GW_GROUP_MIN 256
+#endif
+template <typename PosT>
+static void rsgw_decode_launch(const RsGenTables *tab, const RsGenParams *prm, uint8_t *data, size_t dstride,
+                               uint8_t *parity, size_t pstride, size_t count, const uint16_t *ext, size_t ext_stride,
+                               const PosT *pos, size_t pos_stride, const uint8_t *cnt, uint8_t *ok, uint8_t *corrected,
+                               const uint32_t *list, const uint32_t *list_n, uint32_t *flag, uint32_t seq, int num_cu,
+                               hipStream_t stream)
+{
+    /* a list: the grid for up to 1/16 of the batch, looping past it */
+    const size_t units = list ? (count + 15) / 16 : count;
+    const uint32_t gl = (list || count < GW_GROUP_MIN) ? 64u : prm->nn <= 63u ? 16u : prm->nn <= 127u ? 32u : 64u;
+    const dim3 grid = gw_grid((units * gl + 63u) / 64u, num_cu);
+    if (gl == 16u)
+        RS_LAUNCH((rsgw_decode_k<PosT, 16>), grid, dim3(GW_WG), 0, stream, tab, *prm, data, dstride, parity, pstride,
+                  count, ext, ext_stride, pos, pos_stride, cnt, ok, corrected, list, list_n, flag, seq);
+    else if (gl == 32u)
+        RS_LAUNCH((rsgw_decode_k<PosT, 32>), grid, dim3(GW_WG), 0, stream, tab, *prm, data, dstride, parity, pstride,
+                  count, ext, ext_stride, pos, pos_stride, cnt, ok, corrected, list, list_n, flag, seq);
+    else
+        RS_LAUNCH((rsgw_decode_k<PosT, 64>), grid, dim3(GW_WG), 0, stream, tab, *prm, data, dstride, parity, pstride,
+                  count, ext, ext_stride, pos, pos_stride, cnt, ok, corrected, list, list_n, flag, seq);
+}
+
 extern "C" hipError_t rsgw_decode(const RsGenTables *tab, const RsGenParams *prm, uint8_t *data, size_t dstride,
                                   uint8_t *parity, size_t pstride, size_t count, const uint16_t *ext, size_t ext_stride,
                                   const uint8_t *pos8, const uint32_t *pos32, size_t pos_stride, const uint8_t *cnt,
@@ -1338,14 +1457,12 @@ extern "C" hipError_t rsgw_decode(const RsGenTables *tab, const RsGenParams *prm
 {
     if (count == 0)
         return hipSuccess;
-    /* a list: the grid for up to 1/16 of the batch, looping past it */
-    const dim3 grid = gw_grid(list ? (count + 15) / 16 : count, num_cu);
     if (pos32)
-        RS_LAUNCH(rsgw_decode_k<uint32_t>, grid, dim3(GW_WG), 0, stream, tab, *prm, data, dstride, parity, pstride,
-                  count, ext, ext_stride, pos32, pos_stride, cnt, ok, corrected, list, list_n, flag, seq);
+        rsgw_decode_launch<uint32_t>(tab, prm, data, dstride, parity, pstride, count, ext, ext_stride, pos32,
+                                     pos_stride, cnt, ok, corrected, list, list_n, flag, seq, num_cu, stream);
     else
-        RS_LAUNCH(rsgw_decode_k<uint8_t>, grid, dim3(GW_WG), 0, stream, tab, *prm, data, dstride, parity, pstride,
-                  count, ext, ext_stride, pos8, pos_stride, cnt, ok, corrected, list, list_n, flag, seq);
+        rsgw_decode_launch<uint8_t>(tab, prm, data, dstride, parity, pstride, count, ext, ext_stride, pos8, pos_stride,
+                                    cnt, ok, corrected, list, list_n, flag, seq, num_cu, stream);
     return hipGetLastError();
 }
 

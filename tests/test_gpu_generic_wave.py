@@ -109,7 +109,7 @@ def test_generic_external_syndromes_vs_oracle(torch_cuda, params, path, monkeypa
     nn = (1 << m) - 1
     k = nn - nr
     rng = np.random.default_rng(nr + 3)
-    n = 200
+    n = 300  # >= GW_GROUP_MIN: short codes on the grouped wave kernel (4 or 2 codewords per wave)
     data, par = _rows(rng, o, n, k, nn)
     cw = np.concatenate([data, par], 1)
     syn = np.zeros((n, nr), np.uint16)

@@ -55,6 +55,19 @@ for step in "$@"; do
         run ab 900 python tools/exp_bench.py $(ls build/*.so) $(ls build/*.so) ;;
     prof) run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- \
         python3 bench.py --no-cpu-baseline --no-host --no-c4 --no-latency --no-mixed --no-general --steps 10 ;;
+    pmcab) # the first two SQ counter groups on each build in build/*.so (decode16 round trip)
+        for so in build/*.so; do
+            b=$(basename $so .so)
+            i=0
+            for grp in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE" \
+                       "SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAIT_ANY" \
+                       "SQ_ACTIVE_INST_LDS SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS"; do
+                POPORON_AMD_LIB=$so run pmcab_${b}_$i 300 rocprofv3 --pmc $grp -d gpurun_out/pmcab_$b/pmc$i -o pmc \
+                    --output-format csv -- python3 tools/kernel_driver.py --reps 3
+                i=$((i+1))
+            done
+            python3 tools/pmc_summary.py gpurun_out/pmcab_$b > gpurun_out/pmcab_$b.txt 2>&1
+        done ;;
     pmc_era)
         # the erasure / errata kernels: the same counter groups on the driver's erasure and errata modes
         i=0

@@ -38,7 +38,7 @@ def short(name):
     m = re.search(r"(rs_[a-z_]+<[^>]*>)", name)
     if m:
         return m.group(1)
-    m = re.search(r"\b(rs_(?:bm|chien|forney|apply|era_bp|ebm|chien32|forney32)_k)\b", name)
+    m = re.search(r"\b(rs_(?:bm|bmp|chien|forney|apply|era_bp|ebm|chien32|forney32)_k)\b", name)
     return m.group(1) if m else None
 
 

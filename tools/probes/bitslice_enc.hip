@@ -11,7 +11,7 @@
  * block in registers (two v_perm byte stages, three shift/bitop3 stages): the
  * 32 message planes of 4 steps.  The LFSR's 256 state planes live in a ring
  * of registers and one revolution of 32 steps is generated code
- * (tools/probes/gen_bitslice.py -> bs_net.h: 8 + 22 + 256 VALU ops a step).
+ * (tools/probes/gen_bitslice.py -> bs_net.h, generated on demand and not committed: 8 + 22 + 256 VALU ops a step).
  * A zero byte is prepended to the message (224 steps = 7 revolutions; a
  * leading zero leaves the parity unchanged), so the ring ends unrotated.
  * At the end the 256 planes are transposed back and stored as 8 dwords per
