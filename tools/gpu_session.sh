@@ -55,6 +55,18 @@ for step in "$@"; do
         run ab 900 python tools/exp_bench.py $(ls build/*.so) $(ls build/*.so) ;;
     prof) run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- \
         python3 bench.py --no-cpu-baseline --no-host --no-c4 --no-latency --no-mixed --no-general --steps 10 ;;
+    gwtests) run gw_tests 400 python -u -m pytest tests/test_gpu_generic_wave.py -x -q --timeout 120 --timeout-method thread ;;
+    glat) run glat_wave 300 python tools/general_lat.py --calls 30 --path wave
+          run glat_lane 300 python tools/general_lat.py --calls 30 --path lane ;;
+    gwbatch) # general-parameter batch decodes: both families, then PMC of the wave family on RS(255,155)
+        for prm in 8,0x11d,1,1,100 4,0x13,1,2,8 6,0x43,1,1,10 7,0x89,1,1,20; do
+            for fam in wave lane; do
+                POPORON_AMD_GENERIC=$fam run gwb_${fam}_${prm//,/_} 120 python tools/gw_batch.py --params $prm
+            done
+        done
+        POPORON_AMD_GENERIC=wave run gwb_pmc 200 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_WAVE_CYCLES \
+            SQ_BUSY_CYCLES SQ_WAIT_INST_LDS SQ_ACTIVE_INST_VALU SQ_WAIT_ANY GRBM_GUI_ACTIVE -d gpurun_out/gwb_pmc \
+            -o pmc --output-format csv -- python3 tools/gw_batch.py --params 8,0x11d,1,1,100 --reps 3 ;;
     pmcab) # the first two SQ counter groups on each build in build/*.so (decode16 round trip)
         for so in build/*.so; do
             b=$(basename $so .so)
