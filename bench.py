@@ -244,6 +244,15 @@ class Ranks:
             self.dist.all_reduce(t, op=self.dist.ReduceOp.SUM)
         return int(t.item())
 
+    def gather(self, xs, dtype):
+        """every rank's list xs (same length on every rank), in rank order"""
+        t = self.torch.tensor(list(xs), dtype=dtype, device=self.device)
+        if self.world == 1:
+            return [t.tolist()]
+        out = [self.torch.zeros_like(t) for _ in range(self.world)]
+        self.dist.all_gather(out, t)
+        return [o.tolist() for o in out]
+
     def sum_u64(self, x):
         """sum mod 2^64 of unsigned 64-bit values (carried as two's-complement int64)"""
         v = int(x) & M64
@@ -419,14 +428,20 @@ def run_strong(be, ranks, args, rank, world):
     t = ranks.max(t_codec)
     cs_in, cs_out = ranks.sum_u64(csum_in), ranks.sum_u64(csum_out)
     nbad = ranks.sum_int(nbad)
+    # each rank's share of the checksum (u64 as two's-complement int64): their
+    # sum mod 2^64 is parity_checksum, the same for every N
+    s64 = lambda v: v - (1 << 64) if v >= (1 << 63) else v  # noqa: E731
+    rank_cs = [[c & M64 for c in r] for r in ranks.gather([s64(csum_in & M64), s64(csum_out & M64)], ranks.torch.int64)]
     return {"total_codewords": args.c4_total, "codewords_per_gpu": hi - lo, "n_gpus": world,
             "cw_per_s": round(args.c4_total / t, 1) if t > 0 else None,
             "GB_per_s": round(args.c4_total * CW_BYTES / t / 1e9, 2) if t > 0 else None,
             "ms": round(t * 1e3, 3), "split": "contiguous ranges [T*r/N, T*(r+1)/N)",
             "timed": f"encode + decode@16 of each rank's range (best of {reps}), max over ranks; "
                      "synthesis, channel and checksums untimed",
-            "verified": nbad == 0 and cs_in == cs_out,
+            "verified": nbad == 0 and cs_in == cs_out and sum(r[1] for r in rank_cs) & M64 == cs_out,
             "parity_checksum": cs_out,
+            "rank_checksums": [{"rank": i, "range": list(shard(args.c4_total, i, world)), "in": r[0], "out": r[1]}
+                               for i, r in enumerate(rank_cs)],
             "_samples": {"configs4_encode": {k: np.concatenate(v) for k, v in senc.items()},
                          "configs4_decode16": {k: np.concatenate(v) for k, v in sdec.items()}}}
 
@@ -1285,6 +1300,11 @@ def main(argv=None):
             per_kernel[P.KERNEL_NAMES[k]] = {"ms_per_step": round(step_ms[k], 4), "avg_ms": round(avg_ms[k], 4),
                                              "launches": n, "codewords_per_launch": int(per_launch[k]),
                                              "cw_per_s_per_gpu": round(B / (step_ms[k] * 1e-3), 1)}
+        if world > 1:  # every rank's kernel times (the line's other kernel figures are rank 0's)
+            ids = sorted(P.KERNEL_NAMES)
+            allr = ranks.gather([w["kt"].get(k, (0.0, 0))[0] / args.steps for k in ids], ranks.torch.float64)
+            line["kernels_per_rank_ms_per_step"] = {P.KERNEL_NAMES[k]: [round(r[i], 4) for r in allr]
+                                                    for i, k in enumerate(ids) if any(r[i] for r in allr)}
         enc_ms = sum(v for k, v in step_ms.items() if k == P.KERNEL_ENCODE)
         dec_ms = sum(v for k, v in step_ms.items() if k != P.KERNEL_ENCODE)
         modes = {"encode": path_roofline("encode", kt, args.steps, B, traffic),

@@ -1025,8 +1025,11 @@ __device__ void gw_decode_one(const SM &sm, WT &W, const RsGenParams &P, const G
 /* Full decode, one codeword per GL lanes (rsg_decode_k's modes: ext /
  * erasure slots / errors; list mode): GL = 64 one codeword per wave, 32 / 16
  * two / four per wave for codes of up to 127 / 63 symbols */
+#ifndef GW_WAVES
+#define GW_WAVES 4 /* waves per SIMD the decode kernel is register-bound to (124-128 VGPRs) */
+#endif
 template <typename PosT, int GL>
-__global__ __launch_bounds__(GW_WG, 4) void rsgw_decode_k(const RsGenTables *__restrict__ T, RsGenParams P,
+__global__ __launch_bounds__(GW_WG, GW_WAVES) void rsgw_decode_k(const RsGenTables *__restrict__ T, RsGenParams P,
                                                            uint8_t *data, size_t dstride, uint8_t *parity,
                                                            size_t pstride, size_t count,
                                                            const uint16_t *__restrict__ ext, size_t ext_stride,

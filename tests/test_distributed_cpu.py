@@ -49,6 +49,11 @@ def test_launcher_ranks_and_checksum():
     # configs[4]: the same 1000 codewords however they are split
     assert one["configs4"]["codewords_per_gpu"] == 1000 and two["configs4"]["codewords_per_gpu"] == 500
     assert one["parity_checksum"] == two["parity_checksum"] == one["configs4"]["parity_checksum"]
+    # each rank's share of the checksum, over its own contiguous range
+    rc = two["configs4"]["rank_checksums"]
+    assert [r["range"] for r in rc] == [[0, 500], [500, 1000]]
+    assert sum(r["out"] for r in rc) % (1 << 64) == two["parity_checksum"]
+    assert all(r["in"] == r["out"] for r in rc)  # every rank's range decoded back to its encoded rows
     from oracle import Oracle
     msgs = T.synth_rows_cpu(bench.SEED + 4, 0, 1000, 223)
     cw = np.concatenate([msgs, Oracle().encode_batch(msgs)], 1)

@@ -67,6 +67,17 @@ for step in "$@"; do
         POPORON_AMD_GENERIC=wave run gwb_pmc 200 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_WAVE_CYCLES \
             SQ_BUSY_CYCLES SQ_WAIT_INST_LDS SQ_ACTIVE_INST_VALU SQ_WAIT_ANY GRBM_GUI_ACTIVE -d gpurun_out/gwb_pmc \
             -o pmc --output-format csv -- python3 tools/gw_batch.py --params 8,0x11d,1,1,100 --reps 3 ;;
+    gwab) # general batch decodes on each build in build/*.so (RS(255,155), RS(127,107), RS(15,7)), alternated twice
+        for pass in 1 2; do
+            for so in build/*.so; do
+                for prm in 8,0x11d,1,1,100 7,0x89,1,1,20 4,0x13,1,2,8; do
+                    POPORON_AMD_LIB=$so POPORON_AMD_GENERIC=wave run gwab_$(basename $so .so)_${prm//,/_}_$pass 120 \
+                        python tools/gw_batch.py --params $prm
+                done
+            done
+        done
+        grep -h "M cw/s" gpurun_out/gwab_*.log > gpurun_out/gwab_summary.txt 2>/dev/null
+        for f in gpurun_out/gwab_*.log; do echo "$f: $(grep -h 'M cw/s' $f)"; done > gpurun_out/gwab_summary.txt ;;
     pmcab) # the first two SQ counter groups on each build in build/*.so (decode16 round trip)
         for so in build/*.so; do
             b=$(basename $so .so)
