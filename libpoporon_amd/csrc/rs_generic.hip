@@ -454,15 +454,17 @@ typedef GwRowT<256> GwWave;
 
 struct GwSmem {
     uint8_t alog[256], log[256];
+    uint16_t lgz[256]; /* log with GW_Z for zero */
     uint8_t al2[GW_AL2];
     GwWave w[GW_WG / 64];
 };
 
 /* GL lanes per codeword: 64 / GL codewords per wave (codes of up to 4 GL - 1
- * symbols) */
+ * symbols; GL = 8, 16, 32, 64) */
 template <int GL>
 struct GwSmemG {
     uint8_t alog[256], log[256];
+    uint16_t lgz[256]; /* log with GW_Z for zero */
     uint8_t al2[GW_AL2];
     GwRowT<4 * GL> w[GW_WG / GL];
 };
@@ -520,7 +522,7 @@ __device__ __forceinline__ void gw_shift(const uint32_t (&v)[4], uint32_t (&out)
 }
 
 /* The GL lanes of a wave that share one codeword (GL = 64: the whole wave;
- * 32: a half; 16: a DPP row): the index within the group, the group's bits of
+ * 32: a half; 16: a DPP row; 8: a half-row): the index within the group, the group's bits of
  * a ballot, the XOR over the group and the shift by one index (slot carry
  * from the group's last lane).  Groups run the same code; their branches
  * diverge per codeword. */
@@ -543,6 +545,12 @@ struct GwGrp {
     {
         if constexpr (GL == 64)
             return gw_xor(v);
+        if constexpr (GL == 8) { /* pairs, quads, then the half-row mirror joins the two quads */
+            v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xf, 0xf, false);  /* quad_perm [1,0,3,2] */
+            v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xf, 0xf, false);  /* quad_perm [2,3,0,1] */
+            v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x141, 0xf, 0xf, false); /* row_half_mirror */
+            return v;
+        }
         if constexpr (GL == 32) {
             const auto b = __builtin_amdgcn_permlane16_swap(v, v, false, false);
             v = b[0] ^ b[1];
@@ -571,7 +579,7 @@ struct GwGrp {
                     carry = gb ? t1 : t0;
                 }
             }
-        } else {
+        } else if constexpr (GL == 16) {
             uint32_t carry = first;
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
@@ -579,6 +587,17 @@ struct GwGrp {
                     const uint32_t u = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v[q], 0x121, 0xf, 0xf, false);
                     out[q] = gl ? u : carry; /* row_ror:1: lane 0 sees lane 15, the next slot's carry */
                     carry = u;
+                }
+            }
+        } else { /* GL == 8 */
+            uint32_t carry = first;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                if ((uint32_t)q < nq) {
+                    const uint32_t u = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v[q], 0x111, 0xf, 0xf, true);
+                    const uint32_t hm = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v[q], 0x141, 0xf, 0xf, false);
+                    out[q] = gl ? u : carry; /* row_shr:1; lane 0 of each half-row takes the carry */
+                    carry = hm;              /* row_half_mirror: lane 0 (8) sees lane 7 (15) */
                 }
             }
         }
@@ -599,7 +618,9 @@ __device__ __forceinline__ void gw_tables(SM &sm, const RsGenTables *__restrict_
 {
     for (uint32_t t = threadIdx.x; t < 256u; t += blockDim.x) {
         sm.alog[t] = T->alog[t];
-        sm.log[t] = T->log[t];
+        const uint32_t l = T->log[t];
+        sm.log[t] = (uint8_t)l;
+        sm.lgz[t] = t ? l : GW_Z;
     }
     __syncthreads();
     gw_fill_al2(sm.al2, sm.alog, nn);
@@ -689,6 +710,44 @@ __device__ bool gw_syndromes(const SM &sm, WT &W, const RsGenParams &P, const GM
     return G.any(nz);
 }
 
+/* Berlekamp-Massey, src/decode.c:49-96, over NQ register slots (index i =
+ * gl + GL q): a zero discrepancy (disc = GW_Z) leaves Lambda as it is -- every
+ * product lands on al2's zero region -- and only shifts B, as the
+ * reference's `continue`.  B in GW_Z form; L returns the final length. */
+template <int NQ, int GL, typename SM, typename WT>
+__device__ __forceinline__ void gw_bm(const SM &sm, const WT &W, const GwGrp<GL> &G, uint32_t nr, uint32_t nn,
+                                      uint32_t ne, uint32_t (&lam)[4], uint32_t (&B)[4], uint32_t &L)
+{
+    constexpr uint32_t GLU = GL;
+    const uint16_t *lgz = sm.lgz;
+    const uint8_t *al2 = sm.al2;
+    uint32_t Bm[4];
+    for (uint32_t r = ne + 1u; r <= nr; ++r) {
+        uint32_t part = 0;
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) {
+            const int32_t idx = (int32_t)r - 1 - (int32_t)(G.gl + GLU * q); /* S_(r-1-i); none for i >= r */
+            const uint32_t sv = W.sz[idx > 0 ? idx : 0];
+            part ^= al2[lgz[lam[q]] + (idx >= 0 ? sv : GW_Z)];
+        }
+        const uint32_t dv = G.xr(part);
+        const uint32_t disc = lgz[dv];
+        const bool lengthen = dv != 0u && 2u * L <= r + ne - 1u;
+        G.shift(B, Bm, GW_Z, NQ);
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) {
+            const uint32_t old = lam[q];
+            lam[q] = old ^ al2[disc + Bm[q]];
+            const uint32_t t = lgz[old];
+            const uint32_t v = t + nn - disc;
+            const uint32_t bl = t == GW_Z ? GW_Z : (v >= nn ? v - nn : v);
+            B[q] = lengthen ? bl : Bm[q];
+        }
+        if (lengthen)
+            L = r + ne - L;
+    }
+}
+
 /* src/decode.c:17-230 for the row in W (syndromes in W.S / W.sz): erasure
  * locator, BM, degree, Chien, Omega, Forney, re-syndrome check, apply
  * (in place in data / parity from W.cw).  Same results as g_correct. */
@@ -708,6 +767,12 @@ __device__ bool gw_correct(const SM &sm, WT &W, const RsGenParams &P, const GMod
     for (int q = 0; q < 4; ++q)
         lam[q] = (lane + GLU * q) == 0u ? 1u : 0u;
 
+    /* Sentinel logs: lgz[0] = GW_Z and W.sz use GW_Z for zero, and every sum
+     * with a GW_Z operand indexes al2's zero region (512 + 254 and 1024 are
+     * both >= 2 nn), so no step below branches on a zero operand: each
+     * slot's lookups issue together instead of one guarded chain per slot */
+    const uint16_t *lgz = sm.lgz;
+
     /* erasure locator prod (1 + X_l x), src/decode.c:31-47 */
     if (ne > 0u) {
 #pragma unroll
@@ -722,54 +787,24 @@ __device__ bool gw_correct(const SM &sm, WT &W, const RsGenParams &P, const GMod
             G.shift(lam, Bm, 0u, nq);
 #pragma unroll
             for (int q = 0; q < 4; ++q)
-                if ((uint32_t)q < nq && Bm[q] != 0u)
-                    lam[q] ^= al2[xl + lg[Bm[q]]];
+                if ((uint32_t)q < nq)
+                    lam[q] ^= al2[xl + lgz[Bm[q]]];
         }
     }
 #pragma unroll
     for (int q = 0; q < 4; ++q)
-        B[q] = lg[lam[q]];
+        B[q] = lgz[lam[q]]; /* B in GW_Z form */
 
-    /* Berlekamp-Massey, src/decode.c:49-96 */
+    /* Berlekamp-Massey, src/decode.c:49-96 (gw_bm), the slot count a
+     * compile-time constant so that the slots' lookups issue together */
     uint32_t L = ne;
-    for (uint32_t r = ne + 1u; r <= nr; ++r) {
-        uint32_t part = 0;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const uint32_t i = lane + GLU * q;
-            if ((uint32_t)q < nq && i < r && lam[q] != 0u) {
-                const uint32_t sv = W.S[r - i - 1u];
-                if (sv != A0)
-                    part ^= al2[lg[lam[q]] + sv];
-            }
-        }
-        const uint32_t disc = lg[G.xr(part)];
-        if (disc == A0) {
-            G.shift(B, Bm, A0, nq);
-#pragma unroll
-            for (int q = 0; q < 4; ++q)
-                B[q] = Bm[q];
-            continue;
-        }
-        const bool lengthen = 2u * L <= r + ne - 1u;
-        G.shift(B, Bm, A0, nq);
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            if ((uint32_t)q >= nq)
-                continue;
-            const uint32_t old = lam[q];
-            if (Bm[q] != A0)
-                lam[q] = old ^ al2[disc + Bm[q]];
-            if (lengthen) {
-                const uint32_t v = (uint32_t)lg[old] + nn - disc;
-                B[q] = old == 0u ? A0 : (v >= nn ? v - nn : v);
-            } else {
-                B[q] = Bm[q];
-            }
-        }
-        if (lengthen)
-            L = r + ne - L;
-    }
+    if (nq == 1u)
+        gw_bm<1>(sm, W, G, nr, nn, ne, lam, B, L);
+    else if (nq == 2u)
+        gw_bm<2>(sm, W, G, nr, nn, ne, lam, B, L);
+    else
+        gw_bm<4>(sm, W, G, nr, nn, ne, lam, B, L);
+    (void)Bm;
 
     /* locator to log form, degree, src/decode.c:98-110 */
     uint32_t deg = 0;
@@ -1423,8 +1458,8 @@ extern "C" hipError_t rsgw_encode(const RsGenTables *tab, const RsGenParams *prm
     return hipGetLastError();
 }
 
-/* lanes per codeword of a decode batch: four codewords per wave for codes of
- * up to 63 symbols, two up to 127, from GW_GROUP_MIN codewords on (single
+/* lanes per codeword of a decode batch: eight codewords per wave for codes of
+ * up to 31 symbols, four up to 63, two up to 127, from GW_GROUP_MIN codewords on (single
  * calls and small batches keep the whole wave: the shortest chain per
  * codeword) */
 #ifndef GW_GROUP_MIN
@@ -1439,9 +1474,16 @@ static void rsgw_decode_launch(const RsGenTables *tab, const RsGenParams *prm, u
 {
     /* a list: the grid for up to 1/16 of the batch, looping past it */
     const size_t units = list ? (count + 15) / 16 : count;
-    const uint32_t gl = (list || count < GW_GROUP_MIN) ? 64u : prm->nn <= 63u ? 16u : prm->nn <= 127u ? 32u : 64u;
+    const uint32_t gl = (list || count < GW_GROUP_MIN) ? 64u
+                        : prm->nn <= 31u                  ? 8u
+                        : prm->nn <= 63u                  ? 16u
+                        : prm->nn <= 127u                 ? 32u
+                                                          : 64u;
     const dim3 grid = gw_grid((units * gl + 63u) / 64u, num_cu);
-    if (gl == 16u)
+    if (gl == 8u)
+        RS_LAUNCH((rsgw_decode_k<PosT, 8>), grid, dim3(GW_WG), 0, stream, tab, *prm, data, dstride, parity, pstride,
+                  count, ext, ext_stride, pos, pos_stride, cnt, ok, corrected, list, list_n, flag, seq);
+    else if (gl == 16u)
         RS_LAUNCH((rsgw_decode_k<PosT, 16>), grid, dim3(GW_WG), 0, stream, tab, *prm, data, dstride, parity, pstride,
                   count, ext, ext_stride, pos, pos_stride, cnt, ok, corrected, list, list_n, flag, seq);
     else if (gl == 32u)
