@@ -431,6 +431,9 @@ __global__ __launch_bounds__(G_WG_MAX) void rsg_check_k(const RsGenTables *__res
  * Chien over all points at once, Omega / Forney / the re-syndrome check
  * with lanes over their indices, the apply from an LDS copy of the row. */
 #define GW_WG 256
+#ifndef GW_PHASE_STOP
+#define GW_PHASE_STOP 0 /* experiment builds: 1..7 end the decode before a phase (tools/gw_batch.py --no-check) */
+#endif
 #define GW_Z 512u   /* log of zero in the sentinel arrays: any sum with it indexes al2's zero part */
 #define GW_AL2 1536 /* al2[x] = alpha^(x mod nn) for x < 2 nn, 0 from there on */
 #define GW_QS 16384 /* max size * nr with size + nr <= 255: 127 * 128 (u16: 32 KB) */
@@ -438,7 +441,7 @@ __global__ __launch_bounds__(G_WG_MAX) void rsg_check_k(const RsGenTables *__res
 /* one codeword's LDS state; N = 4 x the lanes per codeword (indices i on
  * lane i % GL, register slot i / GL) */
 template <int N>
-struct GwRowT {
+struct alignas(16) GwRowT {
     uint8_t cw[N];    /* the received row [data | parity], raw bytes */
     uint16_t lr[N];   /* log of each masked byte (GW_Z: zero) */
     uint8_t S[N];     /* syndromes, log form (nn: zero) */
@@ -626,6 +629,32 @@ __device__ __forceinline__ void gw_tables(SM &sm, const RsGenTables *__restrict_
     gw_fill_al2(sm.al2, sm.alog, nn);
 }
 
+/* sv[q] ^= sum over the row's bytes b < total of al2[lr[b] + e_q(b)], e_q
+ * stepping down by sg[q] mod nn per byte: the byte logs read eight at a time
+ * as one 16-byte broadcast (every lane of the group reads the same address;
+ * the row's logs past `total` are GW_Z, so the last chunk needs no guard),
+ * the NQ slots' lookups independent of each other and of the next byte's */
+template <int NQ>
+__device__ __forceinline__ void gw_syn_rows(const uint8_t *al2, const uint16_t *lr, uint32_t total, uint32_t nn,
+                                            uint32_t (&e)[4], const uint32_t (&sg)[4], uint32_t (&sv)[4])
+{
+#pragma unroll 1
+    for (uint32_t b0 = 0; b0 < total; b0 += 8u) {
+        const uint4 v = *reinterpret_cast<const uint4 *>(lr + b0);
+        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const uint32_t l = (w[k >> 1] >> (16 * (k & 1))) & 0xffffu;
+#pragma unroll
+            for (int q = 0; q < NQ; ++q) {
+                sv[q] ^= al2[l + e[q]];
+                const uint32_t t = e[q] - sg[q]; /* e - sg mod nn: the wrapped difference or it plus nn */
+                e[q] = min(t, t + nn);
+            }
+        }
+    }
+}
+
 /* syndromes of the row in W.cw / W.lr into W.S / W.sz; true if any is nonzero
  * (src/decode.c:375-415).  qf: (fcr + nr - 1) prim + nn - 1 < 2^16, so the
  * reference's Horner step multiplies by the constant alpha^((fcr + i) prim
@@ -661,18 +690,20 @@ __device__ bool gw_syndromes(const SM &sm, WT &W, const RsGenParams &P, const GM
             sg[q] = mod(sx * Gr);
             e[q] = g < total ? mod(sx * (total - 1u - g)) : 0u;
         }
-        if (lane < U) {
+        if (Gr > 1u) {
+            if (lane < U) {
 #pragma unroll 4
-            for (uint32_t b = g; b < total; b += Gr) {
-                const uint32_t l = W.lr[b];
-#pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    if ((uint32_t)q < nq && lane + GLU * q < U) { /* q > 0 only for G = 1: the same b for every q */
-                        sv[q] ^= al2[l + e[q]];
-                        e[q] = e[q] >= sg[q] ? e[q] - sg[q] : e[q] + nn - sg[q];
-                    }
+                for (uint32_t b = g; b < total; b += Gr) {
+                    sv[0] ^= al2[W.lr[b] + e[0]];
+                    e[0] = e[0] >= sg[0] ? e[0] - sg[0] : e[0] + nn - sg[0];
                 }
             }
+        } else if (nq == 1u) {
+            gw_syn_rows<1>(al2, W.lr, total, nn, e, sg, sv);
+        } else if (nq == 2u) {
+            gw_syn_rows<2>(al2, W.lr, total, nn, e, sg, sv);
+        } else {
+            gw_syn_rows<4>(al2, W.lr, total, nn, e, sg, sv);
         }
         if (Gr > 1u && lane < U)
             atomicXor(&W.acc[lane % nr], sv[0]);
@@ -708,6 +739,33 @@ __device__ bool gw_syndromes(const SM &sm, WT &W, const RsGenParams &P, const GM
     }
     gw_sync();
     return G.any(nz);
+}
+
+/* Chien sums over NP slots of points: acc[q] ^= sum_(j = 1..deg) al2[lamz[j] +
+ * j pm[q] mod nn], the locator's logs read eight at a time as one 16-byte
+ * broadcast (entries outside 1..deg masked to GW_Z: the array past nr is not
+ * written) */
+template <int NP>
+__device__ __forceinline__ void gw_chien_rows(const uint8_t *al2, const uint16_t *lamz, uint32_t deg, uint32_t nn,
+                                              const uint32_t (&pm)[4], uint32_t (&acc)[4])
+{
+    uint32_t tt[4] = {0, 0, 0, 0}; /* j pm mod nn */
+#pragma unroll 1
+    for (uint32_t j0 = 0; j0 <= deg; j0 += 8u) {
+        const uint4 v = *reinterpret_cast<const uint4 *>(lamz + j0);
+        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const uint32_t j = j0 + (uint32_t)k;
+            const uint32_t lz = (j >= 1u && j <= deg) ? (w[k >> 1] >> (16 * (k & 1))) & 0xffffu : GW_Z;
+#pragma unroll
+            for (int q = 0; q < NP; ++q) {
+                acc[q] ^= al2[lz + tt[q]];
+                const uint32_t t = tt[q] + pm[q];
+                tt[q] = min(t, t - nn); /* t < 2 nn: mod nn (t - nn wraps above t when t < nn) */
+            }
+        }
+    }
 }
 
 /* Berlekamp-Massey, src/decode.c:49-96, over NQ register slots (index i =
@@ -806,6 +864,9 @@ __device__ bool gw_correct(const SM &sm, WT &W, const RsGenParams &P, const GMod
         gw_bm<4>(sm, W, G, nr, nn, ne, lam, B, L);
     (void)Bm;
 
+#if GW_PHASE_STOP == 2 /* experiment builds only: time the phases before this one */
+    return false;
+#endif
     /* locator to log form, degree, src/decode.c:98-110 */
     uint32_t deg = 0;
 #pragma unroll
@@ -823,6 +884,9 @@ __device__ bool gw_correct(const SM &sm, WT &W, const RsGenParams &P, const GMod
         return false;
     gw_sync();
 
+#if GW_PHASE_STOP == 3 /* experiment builds only: time the phases before this one */
+    return false;
+#endif
     /* Chien search, src/decode.c:112-145: point i = lane + 1 + 64 q; the
      * first deg roots in ascending order, the padding check on each */
     {
@@ -835,18 +899,13 @@ __device__ bool gw_correct(const SM &sm, WT &W, const RsGenParams &P, const GMod
             tt[q] = 0;
         }
         const uint32_t np = (nn + GLU - 1u) / GLU; /* slots holding the points 1 .. nn (uniform) */
-#pragma unroll 4
-        for (uint32_t j = 1; j <= deg; ++j) {
-            const uint32_t lz = W.lamz[j];
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                if ((uint32_t)q >= np)
-                    continue;
-                tt[q] += pm[q];
-                tt[q] = tt[q] >= nn ? tt[q] - nn : tt[q];
-                acc[q] ^= al2[lz + tt[q]];
-            }
-        }
+        (void)tt;
+        if (np == 1u)
+            gw_chien_rows<1>(al2, W.lamz, deg, nn, pm, acc);
+        else if (np == 2u)
+            gw_chien_rows<2>(al2, W.lamz, deg, nn, pm, acc);
+        else
+            gw_chien_rows<4>(al2, W.lamz, deg, nn, pm, acc);
         uint32_t base = 0;
         bool padbad = false;
         const uint64_t below = G.below();
@@ -869,6 +928,9 @@ __device__ bool gw_correct(const SM &sm, WT &W, const RsGenParams &P, const GMod
     }
     gw_sync();
 
+#if GW_PHASE_STOP == 4 /* experiment builds only: time the phases before this one */
+    return false;
+#endif
     /* Omega = S Lambda mod x^deg, log form, src/decode.c:147-158 */
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
@@ -883,6 +945,9 @@ __device__ bool gw_correct(const SM &sm, WT &W, const RsGenParams &P, const GMod
     }
     gw_sync();
 
+#if GW_PHASE_STOP == 5 /* experiment builds only: time the phases before this one */
+    return false;
+#endif
     /* Forney, src/decode.c:159-191 (corrected counts nonzero numerators) */
     const uint32_t dtop = (deg < nr - 1u ? deg : nr - 1u) & ~1u;
     uint32_t fixed = 0;
@@ -918,6 +983,9 @@ __device__ bool gw_correct(const SM &sm, WT &W, const RsGenParams &P, const GMod
     corrected = fixed;
     gw_sync();
 
+#if GW_PHASE_STOP == 6 /* experiment builds only: time the phases before this one */
+    return false;
+#endif
     /* re-syndrome check, src/decode.c:193-209 (int16 exponent) */
     {
         bool bad = false;
@@ -941,6 +1009,9 @@ __device__ bool gw_correct(const SM &sm, WT &W, const RsGenParams &P, const GMod
             return false;
     }
 
+#if GW_PHASE_STOP == 7 /* experiment builds only: time the phases before this one */
+    return false;
+#endif
     /* apply, src/decode.c:211-227, from the row's copy in W.cw */
     const uint32_t total = size + nr;
     if (eras_apply) {
@@ -1044,6 +1115,13 @@ __device__ void gw_decode_one(const SM &sm, WT &W, const RsGenParams &P, const G
     } else {
         gw_sync();
         const bool dirty = gw_syndromes(sm, W, P, mod, G, qf);
+#if GW_PHASE_STOP == 1
+        if (okp) { /* experiment builds only */
+            if (lane == 0u)
+                *okp = dirty;
+            return;
+        }
+#endif
         if (pos)
             good = !dirty || (ne <= nr && gw_correct<PosT>(sm, W, P, mod, G, d, par, ne, pos, true, fixed));
         else

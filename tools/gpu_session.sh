@@ -69,7 +69,7 @@ for step in "$@"; do
             -o pmc --output-format csv -- python3 tools/gw_batch.py --params 8,0x11d,1,1,100 --reps 3 ;;
     gwab) # general batch decodes on each build in build/*.so (RS(255,155), RS(127,107), RS(15,7)), alternated twice
         for pass in 1 2; do
-            for so in build/*.so; do
+            for so in build/gw[A-Z]*.so; do
                 for prm in 8,0x11d,1,1,100 7,0x89,1,1,20 4,0x13,1,2,8; do
                     POPORON_AMD_LIB=$so POPORON_AMD_GENERIC=wave run gwab_$(basename $so .so)_${prm//,/_}_$pass 120 \
                         python tools/gw_batch.py --params $prm
@@ -78,6 +78,14 @@ for step in "$@"; do
         done
         grep -h "M cw/s" gpurun_out/gwab_*.log > gpurun_out/gwab_summary.txt 2>/dev/null
         for f in gpurun_out/gwab_*.log; do echo "$f: $(grep -h 'M cw/s' $f)"; done > gpurun_out/gwab_summary.txt ;;
+    gwphase) # general batch decode time up to each phase (build/gwp*.so: GW_PHASE_STOP builds), RS(255,155) and RS(15,7)
+        for so in build/gwp*.so; do
+            for prm in 8,0x11d,1,1,100 4,0x13,1,2,8; do
+                POPORON_AMD_LIB=$so POPORON_AMD_GENERIC=wave run gwp_$(basename $so .so)_${prm//,/_} 120 \
+                    python tools/gw_batch.py --params $prm --no-check
+            done
+        done
+        for f in gpurun_out/gwp_*.log; do echo "$f: $(grep -h 'M cw/s' $f)"; done > gpurun_out/gwphase_summary.txt ;;
     pmcab) # the first two SQ counter groups on each build in build/*.so (decode16 round trip)
         for so in build/*.so; do
             b=$(basename $so .so)

@@ -23,6 +23,7 @@ def main():
     ap.add_argument("--params", default="8,0x11d,1,1,100")
     ap.add_argument("--n", type=int, default=1 << 16)
     ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--no-check", action="store_true", help="experiment builds (GW_PHASE_STOP): skip the result check")
     a = ap.parse_args()
     m, poly, fcr, prim, nr = (int(x, 0) for x in a.params.split(","))
     nn = (1 << m) - 1
@@ -47,7 +48,8 @@ def main():
         h.decode_batch_device(b, nn, b + k, nn, k, a.n, ok.data_ptr(), cor.data_ptr(), stream=s)
         torch.cuda.synchronize()
         ts.append(time.perf_counter() - t0)
-    assert bool((ok == 1).all()) and bool((cor == t).all()), "decode failed"
+    if not a.no_check:
+        assert bool((ok == 1).all()) and bool((cor == t).all()), "decode failed"
     print(f"RS({nn},{k}) n={a.n}: {1e3 * min(ts):.3f} ms best, {a.n / min(ts) / 1e6:.1f} M cw/s")
 
 
