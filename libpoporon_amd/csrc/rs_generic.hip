@@ -470,6 +470,9 @@ struct GwSmemG {
     uint16_t lgz[256]; /* log with GW_Z for zero */
     uint8_t al2[GW_AL2];
     GwRowT<4 * GL> w[GW_WG / GL];
+    uint8_t sideS[GW_WG / GL][4 * GL];   /* gw_decode_pair: the first codeword's syndromes ... */
+    uint16_t sideSz[GW_WG / GL][4 * GL]; /* ... while the row holds the second */
+    uint8_t sideLam[GW_WG / GL][8 * GL]; /* ... and the two locators until each one's finish */
 };
 
 /* lane order within a wave: LDS writes by some lanes, then reads by others */
@@ -772,8 +775,8 @@ __device__ __forceinline__ void gw_chien_rows(const uint8_t *al2, const uint16_t
  * gl + GL q): a zero discrepancy (disc = GW_Z) leaves Lambda as it is -- every
  * product lands on al2's zero region -- and only shifts B, as the
  * reference's `continue`.  B in GW_Z form; L returns the final length. */
-template <int NQ, int GL, typename SM, typename WT>
-__device__ __forceinline__ void gw_bm(const SM &sm, const WT &W, const GwGrp<GL> &G, uint32_t nr, uint32_t nn,
+template <int NQ, int GL, typename SM>
+__device__ __forceinline__ void gw_bm(const SM &sm, const uint16_t *sz, const GwGrp<GL> &G, uint32_t nr, uint32_t nn,
                                       uint32_t ne, uint32_t (&lam)[4], uint32_t (&B)[4], uint32_t &L)
 {
     constexpr uint32_t GLU = GL;
@@ -785,7 +788,7 @@ __device__ __forceinline__ void gw_bm(const SM &sm, const WT &W, const GwGrp<GL>
 #pragma unroll
         for (int q = 0; q < NQ; ++q) {
             const int32_t idx = (int32_t)r - 1 - (int32_t)(G.gl + GLU * q); /* S_(r-1-i); none for i >= r */
-            const uint32_t sv = W.sz[idx > 0 ? idx : 0];
+            const uint32_t sv = sz[idx > 0 ? idx : 0];
             part ^= al2[lgz[lam[q]] + (idx >= 0 ? sv : GW_Z)];
         }
         const uint32_t dv = G.xr(part);
@@ -809,10 +812,61 @@ __device__ __forceinline__ void gw_bm(const SM &sm, const WT &W, const GwGrp<GL>
 /* src/decode.c:17-230 for the row in W (syndromes in W.S / W.sz): erasure
  * locator, BM, degree, Chien, Omega, Forney, re-syndrome check, apply
  * (in place in data / parity from W.cw).  Same results as g_correct. */
+/* gw_bm for two codewords at once (errors mode, ne = 0), their iterations
+ * interleaved in one instruction stream: every step of one codeword's chain
+ * (lookups, the group XOR, the B shift) has the other's beside it, so the
+ * wave waits on half as many latencies per codeword (long codes, whose
+ * nr serial iterations bound a lone wave) */
+template <int NQ, int GL, typename SM>
+__device__ __forceinline__ void gw_bm2(const SM &sm, const uint16_t *szA, const uint16_t *szB, const GwGrp<GL> &G,
+                                       uint32_t nr, uint32_t nn, uint32_t (&lamA)[4], uint32_t (&BA)[4],
+                                       uint32_t (&lamB)[4], uint32_t (&BB)[4])
+{
+    constexpr uint32_t GLU = GL;
+    const uint16_t *lgz = sm.lgz;
+    const uint8_t *al2 = sm.al2;
+    uint32_t BmA[4], BmB[4], LA = 0, LB = 0;
+    for (uint32_t r = 1; r <= nr; ++r) {
+        uint32_t pa = 0, pb = 0;
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) {
+            const int32_t idx = (int32_t)r - 1 - (int32_t)(G.gl + GLU * q);
+            const uint32_t ix = idx > 0 ? (uint32_t)idx : 0u;
+            const uint32_t sa = szA[ix], sb = szB[ix];
+            pa ^= al2[lgz[lamA[q]] + (idx >= 0 ? sa : GW_Z)];
+            pb ^= al2[lgz[lamB[q]] + (idx >= 0 ? sb : GW_Z)];
+        }
+        const uint32_t dva = G.xr(pa), dvb = G.xr(pb);
+        const uint32_t da = lgz[dva], db = lgz[dvb];
+        const bool la = dva != 0u && 2u * LA <= r - 1u, lb = dvb != 0u && 2u * LB <= r - 1u;
+        G.shift(BA, BmA, GW_Z, NQ);
+        G.shift(BB, BmB, GW_Z, NQ);
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) {
+            const uint32_t oa = lamA[q], ob = lamB[q];
+            lamA[q] = oa ^ al2[da + BmA[q]];
+            lamB[q] = ob ^ al2[db + BmB[q]];
+            const uint32_t ta = lgz[oa], tb = lgz[ob];
+            const uint32_t va = ta + nn - da, vb = tb + nn - db;
+            const uint32_t ba = ta == GW_Z ? GW_Z : (va >= nn ? va - nn : va);
+            const uint32_t bb = tb == GW_Z ? GW_Z : (vb >= nn ? vb - nn : vb);
+            BA[q] = la ? ba : BmA[q];
+            BB[q] = lb ? bb : BmB[q];
+        }
+        if (la)
+            LA = r - LA;
+        if (lb)
+            LB = r - LB;
+    }
+}
+
+/* src/decode.c:98-230 after Berlekamp-Massey, for the locator lam (values,
+ * index i = gl + GL q): degree, Chien, Omega, Forney, re-syndrome check,
+ * apply (in place in data / parity from W.cw) */
 template <typename PosT, int GL, typename SM, typename WT>
-__device__ bool gw_correct(const SM &sm, WT &W, const RsGenParams &P, const GMod &mod, const GwGrp<GL> &G,
-                           uint8_t *data, uint8_t *parity, uint32_t ne, const PosT *pos, bool eras_apply,
-                           uint32_t &corrected)
+__device__ bool gw_finish(const SM &sm, WT &W, const RsGenParams &P, const GMod &mod, const GwGrp<GL> &G,
+                          uint8_t *data, uint8_t *parity, const PosT *pos, bool eras_apply, uint32_t &corrected,
+                          const uint32_t (&lam)[4])
 {
     constexpr uint32_t GLU = GL;
     const uint32_t lane = G.gl;
@@ -820,50 +874,6 @@ __device__ bool gw_correct(const SM &sm, WT &W, const RsGenParams &P, const GMod
     const int32_t pad = P.pad;
     const uint8_t *alog = sm.alog, *lg = sm.log, *al2 = sm.al2;
     const uint32_t nq = (nr + GLU) / GLU; /* register slots holding indices 0 .. nr (uniform) */
-    uint32_t lam[4], B[4], Bm[4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q)
-        lam[q] = (lane + GLU * q) == 0u ? 1u : 0u;
-
-    /* Sentinel logs: lgz[0] = GW_Z and W.sz use GW_Z for zero, and every sum
-     * with a GW_Z operand indexes al2's zero region (512 + 254 and 1024 are
-     * both >= 2 nn), so no step below branches on a zero operand: each
-     * slot's lookups issue together instead of one guarded chain per slot */
-    const uint16_t *lgz = sm.lgz;
-
-    /* erasure locator prod (1 + X_l x), src/decode.c:31-47 */
-    if (ne > 0u) {
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const uint32_t i = lane + GLU * q;
-            if (i < ne)
-                W.acc[i] = (uint32_t)pos[i];
-        }
-        gw_sync();
-        for (uint32_t e = 0; e < ne; ++e) {
-            const uint32_t xl = mod(P.prim * (A0 - 1u - (W.acc[e] + (uint32_t)pad)));
-            G.shift(lam, Bm, 0u, nq);
-#pragma unroll
-            for (int q = 0; q < 4; ++q)
-                if ((uint32_t)q < nq)
-                    lam[q] ^= al2[xl + lgz[Bm[q]]];
-        }
-    }
-#pragma unroll
-    for (int q = 0; q < 4; ++q)
-        B[q] = lgz[lam[q]]; /* B in GW_Z form */
-
-    /* Berlekamp-Massey, src/decode.c:49-96 (gw_bm), the slot count a
-     * compile-time constant so that the slots' lookups issue together */
-    uint32_t L = ne;
-    if (nq == 1u)
-        gw_bm<1>(sm, W, G, nr, nn, ne, lam, B, L);
-    else if (nq == 2u)
-        gw_bm<2>(sm, W, G, nr, nn, ne, lam, B, L);
-    else
-        gw_bm<4>(sm, W, G, nr, nn, ne, lam, B, L);
-    (void)Bm;
-
 #if GW_PHASE_STOP == 2 /* experiment builds only: time the phases before this one */
     return false;
 #endif
@@ -1073,6 +1083,63 @@ __device__ bool gw_correct(const SM &sm, WT &W, const RsGenParams &P, const GMod
     return first_bad == deg;
 }
 
+template <typename PosT, int GL, typename SM, typename WT>
+__device__ bool gw_correct(const SM &sm, WT &W, const RsGenParams &P, const GMod &mod, const GwGrp<GL> &G,
+                           uint8_t *data, uint8_t *parity, uint32_t ne, const PosT *pos, bool eras_apply,
+                           uint32_t &corrected)
+{
+    constexpr uint32_t GLU = GL;
+    const uint32_t lane = G.gl;
+    const uint32_t nr = P.nroots, nn = P.nn, A0 = P.nn;
+    const int32_t pad = P.pad;
+    const uint8_t *al2 = sm.al2;
+    const uint32_t nq = (nr + GLU) / GLU; /* register slots holding indices 0 .. nr (uniform) */
+    uint32_t lam[4], B[4], Bm[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+        lam[q] = (lane + GLU * q) == 0u ? 1u : 0u;
+
+    /* Sentinel logs: lgz[0] = GW_Z and W.sz use GW_Z for zero, and every sum
+     * with a GW_Z operand indexes al2's zero region (512 + 254 and 1024 are
+     * both >= 2 nn), so no step below branches on a zero operand: each
+     * slot's lookups issue together instead of one guarded chain per slot */
+    const uint16_t *lgz = sm.lgz;
+
+    /* erasure locator prod (1 + X_l x), src/decode.c:31-47 */
+    if (ne > 0u) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const uint32_t i = lane + GLU * q;
+            if (i < ne)
+                W.acc[i] = (uint32_t)pos[i];
+        }
+        gw_sync();
+        for (uint32_t e = 0; e < ne; ++e) {
+            const uint32_t xl = mod(P.prim * (A0 - 1u - (W.acc[e] + (uint32_t)pad)));
+            G.shift(lam, Bm, 0u, nq);
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+                if ((uint32_t)q < nq)
+                    lam[q] ^= al2[xl + lgz[Bm[q]]];
+        }
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+        B[q] = lgz[lam[q]]; /* B in GW_Z form */
+
+    /* Berlekamp-Massey, src/decode.c:49-96 (gw_bm), the slot count a
+     * compile-time constant so that the slots' lookups issue together */
+    uint32_t L = ne;
+    if (nq == 1u)
+        gw_bm<1>(sm, W.sz, G, nr, nn, ne, lam, B, L);
+    else if (nq == 2u)
+        gw_bm<2>(sm, W.sz, G, nr, nn, ne, lam, B, L);
+    else
+        gw_bm<4>(sm, W.sz, G, nr, nn, ne, lam, B, L);
+    (void)Bm;
+    return gw_finish<PosT>(sm, W, P, mod, G, data, parity, pos, eras_apply, corrected, lam);
+}
+
 /* One codeword on one wave, branch logic of src/decode.c:431-487: x (the
  * row's external log-form syndromes) or pos / ne (its erasure slots and
  * count) or neither; ok / corrected_num to okp / corp (corp may be NULL) */
@@ -1135,9 +1202,127 @@ __device__ void gw_decode_one(const SM &sm, WT &W, const RsGenParams &P, const G
     gw_sync();
 }
 
+/* the row [data | parity] of one codeword into W.cw (and its logs into W.lr) */
+template <int GL, typename SM, typename WT>
+__device__ __forceinline__ void gw_load_row(const SM &sm, WT &W, const RsGenParams &P, const GwGrp<GL> &G,
+                                            const uint8_t *d, const uint8_t *par, bool logs)
+{
+    constexpr uint32_t GLU = GL;
+    const uint32_t size = P.size, total = size + P.nroots;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const uint32_t b = G.gl + GLU * q;
+        const uint32_t v = b < size ? d[b] : (b < total ? par[b - size] : 0u);
+        const uint32_t m = v & P.nn;
+        W.cw[b] = (uint8_t)v;
+        if (logs)
+            W.lr[b] = m ? (uint32_t)sm.log[m] : GW_Z;
+    }
+}
+
+/* Two codewords on one wave, errors mode (no erasure list, no external
+ * syndromes), nroots < 2 GL: syndromes of A (kept in the side buffer) and of
+ * B (in the row), Berlekamp-Massey of both interleaved (gw_bm2), then the
+ * rest for B and, with A's row reloaded and its syndromes restored, for A.
+ * Same results as gw_decode_one on each. */
+template <int GL, typename SM, typename WT>
+__device__ void gw_decode_pair(const SM &sm, WT &W, uint8_t *sideS, uint16_t *sideSz, uint8_t *sideLam,
+                               const RsGenParams &P,
+                               const GMod &mod, const GwGrp<GL> &G, bool qf, uint8_t *dA, uint8_t *pA, uint8_t *okA,
+                               uint8_t *corA, uint8_t *dB, uint8_t *pB, uint8_t *okB, uint8_t *corB)
+{
+    constexpr uint32_t GLU = GL;
+    const uint32_t nr = P.nroots, nq = (nr + GLU) / GLU;
+    const uint32_t lane = G.gl;
+    gw_load_row(sm, W, P, G, dA, pA, true);
+    gw_sync();
+    const bool dirtyA = gw_syndromes(sm, W, P, mod, G, qf);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const uint32_t i = lane + GLU * q;
+        if (i < nr) {
+            sideS[i] = W.S[i];
+            sideSz[i] = W.sz[i];
+        }
+    }
+    gw_load_row(sm, W, P, G, dB, pB, true);
+    gw_sync();
+    const bool dirtyB = gw_syndromes(sm, W, P, mod, G, qf);
+    /* Berlekamp-Massey of the dirty ones (both: interleaved), each locator
+     * parked in LDS, then one finish per dirty codeword: B (in the row), then
+     * A with its row reloaded and its syndromes restored */
+    uint32_t lam[4], Bl[4];
+    if (dirtyA || dirtyB) {
+        uint32_t lamB[4], BB[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            lam[q] = lamB[q] = (lane + GLU * q) == 0u ? 1u : 0u;
+            Bl[q] = BB[q] = sm.lgz[lam[q]];
+        }
+        uint32_t L = 0;
+        if (dirtyA && dirtyB) {
+            if (nq == 1u)
+                gw_bm2<1>(sm, sideSz, W.sz, G, nr, P.nn, lam, Bl, lamB, BB);
+            else
+                gw_bm2<2>(sm, sideSz, W.sz, G, nr, P.nn, lam, Bl, lamB, BB);
+        } else if (nq == 1u) {
+            gw_bm<1>(sm, dirtyA ? sideSz : W.sz, G, nr, P.nn, 0u, dirtyA ? lam : lamB, dirtyA ? Bl : BB, L);
+        } else {
+            gw_bm<2>(sm, dirtyA ? sideSz : W.sz, G, nr, P.nn, 0u, dirtyA ? lam : lamB, dirtyA ? Bl : BB, L);
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            sideLam[lane + GLU * q] = (uint8_t)lam[q];
+            sideLam[4u * GLU + lane + GLU * q] = (uint8_t)lamB[q];
+        }
+    }
+    uint32_t fixA = 0, fixB = 0;
+    bool goodA = true, goodB = true;
+#pragma unroll 1
+    for (int k = 0; k < 2; ++k) { /* k = 0: B, 1: A */
+        if (k == 0 ? !dirtyB : !dirtyA)
+            continue;
+        if (k == 1) { /* the row holds B: A's bytes and syndromes back */
+            gw_sync();
+            gw_load_row(sm, W, P, G, dA, pA, false);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const uint32_t i = lane + GLU * q;
+                if (i < nr) {
+                    W.S[i] = sideS[i];
+                    W.sz[i] = sideSz[i];
+                }
+            }
+        }
+        gw_sync();
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+            lam[q] = sideLam[(k == 0 ? 4u * GLU : 0u) + lane + GLU * q];
+        uint32_t fix = 0;
+        const bool good = gw_finish<uint8_t>(sm, W, P, mod, G, k == 0 ? dB : dA, k == 0 ? pB : pA,
+                                             (const uint8_t *)nullptr, false, fix, lam);
+        if (k == 0)
+            goodB = good, fixB = fix;
+        else
+            goodA = good, fixA = fix;
+    }
+    if (lane == 0u) {
+        *okA = goodA ? 1 : 0;
+        *okB = goodB ? 1 : 0;
+        if (corA) {
+            *corA = (uint8_t)fixA;
+            *corB = (uint8_t)fixB;
+        }
+    }
+    gw_sync();
+}
+
 /* Full decode, one codeword per GL lanes (rsg_decode_k's modes: ext /
  * erasure slots / errors; list mode): GL = 64 one codeword per wave, 32 / 16
  * two / four per wave for codes of up to 127 / 63 symbols */
+#ifndef GW_PAIR
+#define GW_PAIR 1 /* rsgw_decode_k<., 64>: two codewords per pass in errors mode (gw_decode_pair) */
+#endif
 #ifndef GW_WAVES
 #define GW_WAVES 4 /* waves per SIMD the decode kernel is register-bound to (124-128 VGPRs) */
 #endif
@@ -1166,8 +1351,20 @@ __global__ __launch_bounds__(GW_WG, GW_WAVES) void rsgw_decode_k(const RsGenTabl
     auto &W = sm.w[slot];
     const GMod mod{P.nn, P.magic};
     const bool qf = (P.fcr + P.nroots - 1u) * P.prim + P.nn - 1u < 65536u;
-    for (size_t e = (size_t)blockIdx.x * CPB + slot; e < n; e += (size_t)gridDim.x * CPB) {
+    const size_t stride = (size_t)gridDim.x * CPB;
+    /* long codes in errors mode: two codewords per pass, their BM interleaved */
+    const bool pair = GL == 64 && GW_PAIR && !ext && !pos && P.nroots < 2u * GL && P.nroots >= 8u;
+    for (size_t e = (size_t)blockIdx.x * CPB + slot; e < n; e += pair ? 2u * stride : stride) {
         const size_t cw = list ? (size_t)list[e] : e;
+        if (pair && e + stride < n) {
+            const size_t c2 = list ? (size_t)list[e + stride] : e + stride;
+            gw_decode_pair<GL>(sm, W, sm.sideS[slot], sm.sideSz[slot], sm.sideLam[slot], P, mod, G, qf,
+                               data + cw * dstride,
+                               parity + cw * pstride, ok + cw, corrected ? corrected + cw : nullptr,
+                               data + c2 * dstride, parity + c2 * pstride, ok + c2,
+                               corrected ? corrected + c2 : nullptr);
+            continue;
+        }
         gw_decode_one<PosT, GL>(sm, W, P, mod, G, qf, data + cw * dstride, parity + cw * pstride,
                                 ext ? ext + cw * ext_stride : nullptr, pos ? pos + cw * pos_stride : nullptr,
                                 pos ? (uint32_t)cntv[cw] : 0u, ok + cw, corrected ? corrected + cw : nullptr);

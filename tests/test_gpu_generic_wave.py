@@ -341,3 +341,40 @@ def test_generic_large_batch_round_trip(torch_cuda, params):
     ook, ocor, od, op = o.decode_batch(bad[idx, :k], bad[idx, k:])
     assert (ook == 1).all() and (ocor == t).all() and (od == clean[idx, :k]).all() and (op == clean[idx, k:]).all()
     h.close()
+
+
+@pytest.mark.parametrize("params", [(8, 0x11D, 1, 1, 100), (8, 0x187, 5, 7, 48), (8, 0x11D, 2000, 37, 32)])
+def test_generic_pair_batches_vs_oracle(torch_cuda, params):
+    """Batches large enough that each wave of rsgw_decode_k<., 64> takes two
+    codewords per pass (gw_decode_pair: the first's syndromes kept aside,
+    both Berlekamp-Massey runs interleaved, B finished before A), with every
+    case mixed in: clean rows, 1..t errors, t+1..t+3 (the reference's
+    failures and miscorrections) -- every row's bytes, ok and corrected_num
+    against the oracle."""
+    from oracle import Oracle
+    torch = torch_cuda
+    m, poly, fcr, prim, nr = params
+    nn = (1 << m) - 1
+    k, t = nn - nr, nr // 2
+    n = 20000  # > the 8,192 waves of a capped grid: passes pair codewords e and e + 8192
+    o, h = Oracle(*params), P.Poporon(*params)
+    rng = np.random.default_rng(nr * 7 + fcr)
+    data = rng.integers(0, nn + 1, (n, k), dtype=np.uint8)
+    cw = np.concatenate([data, o.encode_batch(data)], 1)
+    ne = rng.integers(0, t + 4, n)
+    ne[rng.random(n) < 0.2] = 0  # clean rows beside dirty ones in the same pass
+    for c in range(n):
+        p = rng.permutation(nn)[:ne[c]]
+        cw[c, p] ^= rng.integers(1, nn + 1, ne[c]).astype(np.uint8)
+    rows = torch.from_numpy(cw).cuda()
+    ok = torch.zeros(n, dtype=torch.uint8, device="cuda")
+    cor = torch.zeros(n, dtype=torch.uint8, device="cuda")
+    b = rows.data_ptr()
+    h.decode_batch_device(b, nn, b + k, nn, k, n, ok.data_ptr(), cor.data_ptr(),
+                          stream=torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    got = rows.cpu().numpy()
+    ook, ocor, od, op = o.decode_batch(cw[:, :k], cw[:, k:])
+    assert (ok.cpu().numpy() == ook).all() and (cor.cpu().numpy() == ocor).all()
+    assert (got[:, :k] == od).all() and (got[:, k:] == op).all()
+    h.close()
