@@ -1044,7 +1044,7 @@ def general_wave(be, sets=((8, 0x11D, 1, 1, 100), (4, 0x13, 1, 2, 8)), n=1 << 16
         buf = src.clone()
         ok, cor = be.status(n)
         b = buf.data_ptr()
-        tb = []
+        tb, tk = [], []
         for r in range(reps + 1):
             buf.copy_(src)
             be.sync()
@@ -1053,21 +1053,33 @@ def general_wave(be, sets=((8, 0x11D, 1, 1, 100), (4, 0x13, 1, 2, 8)), n=1 << 16
             be.sync()
             if r:
                 tb.append(time.perf_counter() - t0)
+        for r in range(reps):  # device time: the stream kept busy while the host enqueues (no launch gap counted)
+            buf.copy_(src)
+            be.sync()
+            torch.cuda._sleep(200000)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            h.decode_batch_device(b, nn, b + k, nn, k, n, ok.data_ptr(), cor.data_ptr(), stream=s)
+            e1.record()
+            be.sync()
+            tk.append(e0.elapsed_time(e1) * 1e-3)
         got, gok, gcor = buf.cpu().numpy(), ok.cpu().numpy(), cor.cpu().numpy()
         idx = np.arange(0, n, 256)
         ook, ocor, od, op = o.decode_batch(bad[idx, :k], bad[idx, k:])
         mism += int(((ook != gok[idx]) | (ocor != gcor[idx]) | (od != got[idx, :k]).any(1) |
                      (op != got[idx, k:]).any(1)).sum())
         mism += int((got != cw).any(1).sum())  # t errors: every codeword back to the encoded row
-        d = float(np.median(tb))
+        d, dk = float(np.median(tb)), float(np.median(tk))
         out[f"RS({nn},{k})"] = {
             "params": {"symbol_size": m, "poly": hex(poly), "fcr": fcr, "prim": prim, "num_roots": nr},
             "single_encode_us": round(te * 1e6, 1), "single_decode_us": round(td * 1e6, 1),
             "batch_codewords": n, "batch_decode_cw_per_s": round(n / d, 1), "batch_decode_ms": round(d * 1e3, 4),
+            "batch_decode_device_cw_per_s": round(n / dk, 1), "batch_decode_device_ms": round(dk * 1e3, 4),
             "errors_per_codeword": t, "mismatches": mism}
         h.close()
     out["note"] = ("single calls: poporon_encode / poporon_decode through ctypes (one wave, coherent host memory); "
-                   "batch: poporon_decode_batch_device, wall time; checked against oracle/rs_oracle.c")
+                   "batch: poporon_decode_batch_device, wall time of the Python call (batch_decode_*) and device "
+                   "time between HIP events on its stream (batch_decode_device_*); checked against oracle/rs_oracle.c")
     out["verified"] = all(v["mismatches"] == 0 for kk, v in out.items() if isinstance(v, dict))
     return out
 
