@@ -1373,13 +1373,16 @@ static bool rem_release(GpuCtx &g, hipStream_t s)
     return true;
 }
 
-/* general parameters: one codeword per wave (rsgw_*) or per lane (rsg_*).
- * The wave kernels take single calls and batches below 16,384 codewords of
- * every code (a few us to ~0.35 ms per call against 20 us to 24 ms), and
- * large batches of long codes: decode from 127-symbol codewords, encode of
- * 255-symbol ones.  Large batches of short codes keep one codeword per lane
- * (65,536 codewords of 2^m - 1 = 63 / 31 / 15: 213 / 84 / 79 us against 242
- * / 172 / 201 us per decode call; profiles/r05_general_lat_*.log) */
+/* general parameters: one codeword per 8..64 lanes (rsgw_*) or per lane
+ * (rsg_*).  The wave kernels take single calls and batches below 16,384
+ * codewords of every code, every large decode batch of codes of 15 symbols
+ * or more (round 6: 8 / 16 / 32 lanes per codeword for codes of up to 31 /
+ * 63 / 127 symbols, branch-free BM; 65,536 codewords of 2^m - 1 = 15 / 31 /
+ * 63 / 127: 40 / 39 / 70 / 184 us against 80 / 84 / 213 / 745 us per lane,
+ * profiles/r06_general_lat_{wave,lane}.log) and large encode batches of
+ * 255-symbol codes; the per-lane kernels large decode batches of 3- and
+ * 7-symbol codes (22 us vs 32 at m = 2) and large encode batches of shorter
+ * codes (one LFSR per lane: 17-217 us vs 29-274) */
 static bool gen_wave(const poporon_t *h, size_t count, bool encode, size_t size)
 {
     const uint32_t nn = h->rs->gf->field_size;
@@ -1387,7 +1390,7 @@ static bool gen_wave(const poporon_t *h, size_t count, bool encode, size_t size)
         return false;
     if (h->gen_path)
         return h->gen_path == 2;
-    return count < 16384 || (encode ? nn == 255u : nn >= 127u);
+    return count < 16384 || (encode ? nn == 255u : nn >= 15u);
 }
 
 static bool launch_encode(poporon_t *h, const uint8_t *d_data, size_t ds, uint8_t *d_par, size_t ps, size_t size,

@@ -302,10 +302,12 @@ def test_generic_single_call_server_vs_oracle(params):
 
 
 @pytest.mark.parametrize("params", [(8, 0x11D, 1, 1, 100), (4, 0x13, 1, 2, 8), (7, 0x89, 1, 1, 20),
-                                    (6, 0x43, 1, 1, 10)])
+                                    (6, 0x43, 1, 1, 10), (5, 0x25, 3, 1, 6), (2, 0x7, 1, 1, 2)])
 def test_generic_large_batch_round_trip(torch_cuda, params):
-    """Large device batches on the default routing (one codeword per wave for
-    long codes, per lane for short ones past 16,384 codewords): 2^18 rows
+    """Large device batches on the default routing (decode: 64 lanes per
+    codeword for 255-symbol codes, two codewords per pass; 32 / 16 / 8 lanes
+    for codes of up to 127 / 63 / 31 symbols; one codeword per lane for
+    3-symbol codes; encode per lane below 255 symbols): 2^18 rows
     encoded, t random errors each, decoded -- every row back to the encoded
     one with ok = 1 and corrected_num = t (a size-independent property), and
     every 1024th row equal to the oracle's encode and decode."""
