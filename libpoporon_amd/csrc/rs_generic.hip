@@ -463,7 +463,7 @@ struct GwSmem {
 };
 
 /* GL lanes per codeword: 64 / GL codewords per wave (codes of up to 4 GL - 1
- * symbols; GL = 8, 16, 32, 64) */
+ * symbols; GL = 4, 8, 16, 32, 64) */
 template <int GL>
 struct GwSmemG {
     uint8_t alog[256], log[256];
@@ -528,7 +528,7 @@ __device__ __forceinline__ void gw_shift(const uint32_t (&v)[4], uint32_t (&out)
 }
 
 /* The GL lanes of a wave that share one codeword (GL = 64: the whole wave;
- * 32: a half; 16: a DPP row; 8: a half-row): the index within the group, the group's bits of
+ * 32: a half; 16: a DPP row; 8: a half-row; 4: a quad): the index within the group, the group's bits of
  * a ballot, the XOR over the group and the shift by one index (slot carry
  * from the group's last lane).  Groups run the same code; their branches
  * diverge per codeword. */
@@ -551,6 +551,11 @@ struct GwGrp {
     {
         if constexpr (GL == 64)
             return gw_xor(v);
+        if constexpr (GL == 4) { /* pairs, then quads */
+            v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xf, 0xf, false); /* quad_perm [1,0,3,2] */
+            v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xf, 0xf, false); /* quad_perm [2,3,0,1] */
+            return v;
+        }
         if constexpr (GL == 8) { /* pairs, quads, then the half-row mirror joins the two quads */
             v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xf, 0xf, false);  /* quad_perm [1,0,3,2] */
             v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xf, 0xf, false);  /* quad_perm [2,3,0,1] */
@@ -592,6 +597,16 @@ struct GwGrp {
                 if ((uint32_t)q < nq) {
                     const uint32_t u = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v[q], 0x121, 0xf, 0xf, false);
                     out[q] = gl ? u : carry; /* row_ror:1: lane 0 sees lane 15, the next slot's carry */
+                    carry = u;
+                }
+            }
+        } else if constexpr (GL == 4) {
+            uint32_t carry = first;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                if ((uint32_t)q < nq) {
+                    const uint32_t u = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v[q], 0x93, 0xf, 0xf, false);
+                    out[q] = gl ? u : carry; /* quad_perm [3,0,1,2]: lane 0 sees lane 3, the next slot's carry */
                     carry = u;
                 }
             }
@@ -1733,8 +1748,9 @@ extern "C" hipError_t rsgw_encode(const RsGenTables *tab, const RsGenParams *prm
     return hipGetLastError();
 }
 
-/* lanes per codeword of a decode batch: eight codewords per wave for codes of
- * up to 31 symbols, four up to 63, two up to 127, from GW_GROUP_MIN codewords on (single
+/* lanes per codeword of a decode batch: sixteen codewords per wave for codes
+ * of up to 15 symbols, eight up to 31, four up to 63, two up to 127, from
+ * GW_GROUP_MIN codewords on (single
  * calls and small batches keep the whole wave: the shortest chain per
  * codeword) */
 #ifndef GW_GROUP_MIN
@@ -1750,12 +1766,16 @@ static void rsgw_decode_launch(const RsGenTables *tab, const RsGenParams *prm, u
     /* a list: the grid for up to 1/16 of the batch, looping past it */
     const size_t units = list ? (count + 15) / 16 : count;
     const uint32_t gl = (list || count < GW_GROUP_MIN) ? 64u
+                        : prm->nn <= 15u                  ? 4u
                         : prm->nn <= 31u                  ? 8u
                         : prm->nn <= 63u                  ? 16u
                         : prm->nn <= 127u                 ? 32u
                                                           : 64u;
     const dim3 grid = gw_grid((units * gl + 63u) / 64u, num_cu);
-    if (gl == 8u)
+    if (gl == 4u)
+        RS_LAUNCH((rsgw_decode_k<PosT, 4>), grid, dim3(GW_WG), 0, stream, tab, *prm, data, dstride, parity, pstride,
+                  count, ext, ext_stride, pos, pos_stride, cnt, ok, corrected, list, list_n, flag, seq);
+    else if (gl == 8u)
         RS_LAUNCH((rsgw_decode_k<PosT, 8>), grid, dim3(GW_WG), 0, stream, tab, *prm, data, dstride, parity, pstride,
                   count, ext, ext_stride, pos, pos_stride, cnt, ok, corrected, list, list_n, flag, seq);
     else if (gl == 16u)
