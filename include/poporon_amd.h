@@ -178,7 +178,11 @@ bool poporon_amd_rng_fill_device(poporon_rng_t *rng, void *d_dest, size_t size, 
  * poporon_amd_multi_create makes one handle per listed device (devices NULL:
  * every visible device) from the same config (copied; erasure / syndrome
  * pointers borrowed as by poporon_create) and initialises each device.  A
- * device may be listed more than once (independent handles sharing it).
+ * device may be listed more than once (independent handles sharing it); each
+ * listing is a full handle with its own streams, device tables (0.3 MB),
+ * split-decode workspace (160 B per codeword of its largest decode batch),
+ * single-call buffers and host-pipeline pinned slots, so repeats multiply
+ * that memory (no cap: the caller chooses the list).
  * The host entry points take the arguments of poporon_encode_batch /
  * poporon_decode_batch and run one host thread per device over its range.
  * The device entry points take per-device pointer arrays: element i points to

@@ -18,6 +18,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
@@ -2493,6 +2494,7 @@ static int srv_call(poporon_t *h, uint32_t op, uint32_t size, uint32_t mode)
  * grid would wait for its idle limit, and with GPU_MAX_HW_QUEUES below the
  * streams in use its dispatch can share a hardware queue with the batch's.
  * The next single call launches a new server. */
+#define SRV_STOP_DEADLINE_S 10
 static bool srv_stop(poporon_t *h)
 {
     GpuCtx &g = h->gpu;
@@ -2503,6 +2505,10 @@ static bool srv_stop(poporon_t *h)
     std::atomic_thread_fence(std::memory_order_release);
     z32[ZC_REQ / 4] = srv_word(g, prev, RS_SRV_STOP, 0u, 0u);
     const volatile uint32_t *ex = z32 + ZC_EXITED / 4;
+    /* a queued server sees the stop request as soon as it runs; past
+     * SRV_STOP_DEADLINE_S (the GPU busy with other work for that long, or
+     * hung) the batch call fails instead of spinning on */
+    const auto t0 = std::chrono::steady_clock::now();
     for (uint32_t spin = 1; *ex != g.srv_id; ++spin) {
         if ((spin & 4095u) == 0u) {
             const hipError_t e = hipStreamQuery(g.sstream);
@@ -2510,6 +2516,8 @@ static bool srv_stop(poporon_t *h)
                 g.srv_on = false;
                 return fail("single-call server ended without its exit word");
             }
+            if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(SRV_STOP_DEADLINE_S))
+                return fail("single-call server did not leave within %d s of a stop request", SRV_STOP_DEADLINE_S);
             if (e != hipSuccess && e != hipErrorNotReady) {
                 g.srv_on = false;
                 return fail("HIP error %d (%s) in the single-call server", (int)e, hipGetErrorString(e));
