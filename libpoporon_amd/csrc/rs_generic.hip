@@ -786,19 +786,43 @@ __device__ __forceinline__ void gw_chien_rows(const uint8_t *al2, const uint16_t
     }
 }
 
-/* Berlekamp-Massey, src/decode.c:49-96, over NQ register slots (index i =
- * gl + GL q): a zero discrepancy (disc = GW_Z) leaves Lambda as it is -- every
- * product lands on al2's zero region -- and only shifts B, as the
- * reference's `continue`.  B in GW_Z form; L returns the final length. */
+#ifndef GW_NARROW
+#define GW_NARROW 1 /* Berlekamp-Massey on fewer register slots while the high ones stay zero (gw_bm narrow) */
+#endif
+
+/* true when some group's B holds a nonzero at index GL NQ - 1 (its last lane,
+ * slot NQ - 1): the next shift would carry it into slot NQ (wave-uniform) */
+template <int NQ, int GL>
+__device__ __forceinline__ bool gw_top_set(const GwGrp<GL> &G, const uint32_t (&B)[4])
+{
+    if constexpr (GL == 64)
+        return (uint32_t)__builtin_amdgcn_readlane((int)B[NQ - 1], 63) != GW_Z;
+    else
+        return __ballot(G.gl == (uint32_t)GL - 1u && B[NQ - 1] != GW_Z) != 0ull;
+}
+
+/* Berlekamp-Massey, src/decode.c:49-96, iterations r0 .. nr over NQ register
+ * slots (index i = gl + GL q): a zero discrepancy (disc = GW_Z) leaves Lambda
+ * as it is -- every product lands on al2's zero region -- and only shifts B,
+ * as the reference's `continue`.  B in GW_Z form; L returns the length.
+ * narrow: the slots from NQ on hold zeros (Lambda 0, B GW_Z) and stay so
+ * while B's top index GL NQ - 1 is zero before a shift (deg Lambda <= L,
+ * deg x B <= r - L: a word with nr / 2 errors keeps both at most nr / 2, so
+ * RS(255,155)'s 100 roots run on one slot of 64); the run stops before the
+ * first iteration whose shift would carry a nonzero out and returns it for
+ * a wider run to continue from (nr + 1: done) */
 template <int NQ, int GL, typename SM>
-__device__ __forceinline__ void gw_bm(const SM &sm, const uint16_t *sz, const GwGrp<GL> &G, uint32_t nr, uint32_t nn,
-                                      uint32_t ne, uint32_t (&lam)[4], uint32_t (&B)[4], uint32_t &L)
+__device__ __forceinline__ uint32_t gw_bm(const SM &sm, const uint16_t *sz, const GwGrp<GL> &G, uint32_t r0,
+                                          uint32_t nr, uint32_t nn, uint32_t ne, bool narrow, uint32_t (&lam)[4],
+                                          uint32_t (&B)[4], uint32_t &L)
 {
     constexpr uint32_t GLU = GL;
     const uint16_t *lgz = sm.lgz;
     const uint8_t *al2 = sm.al2;
     uint32_t Bm[4];
-    for (uint32_t r = ne + 1u; r <= nr; ++r) {
+    for (uint32_t r = r0; r <= nr; ++r) {
+        if (narrow && gw_top_set<NQ>(G, B))
+            return r;
         uint32_t part = 0;
 #pragma unroll
         for (int q = 0; q < NQ; ++q) {
@@ -822,6 +846,7 @@ __device__ __forceinline__ void gw_bm(const SM &sm, const uint16_t *sz, const Gw
         if (lengthen)
             L = r + ne - L;
     }
+    return nr + 1u;
 }
 
 /* src/decode.c:17-230 for the row in W (syndromes in W.S / W.sz): erasure
@@ -833,15 +858,18 @@ __device__ __forceinline__ void gw_bm(const SM &sm, const uint16_t *sz, const Gw
  * wave waits on half as many latencies per codeword (long codes, whose
  * nr serial iterations bound a lone wave) */
 template <int NQ, int GL, typename SM>
-__device__ __forceinline__ void gw_bm2(const SM &sm, const uint16_t *szA, const uint16_t *szB, const GwGrp<GL> &G,
-                                       uint32_t nr, uint32_t nn, uint32_t (&lamA)[4], uint32_t (&BA)[4],
-                                       uint32_t (&lamB)[4], uint32_t (&BB)[4])
+__device__ __forceinline__ uint32_t gw_bm2(const SM &sm, const uint16_t *szA, const uint16_t *szB,
+                                           const GwGrp<GL> &G, uint32_t r0, uint32_t nr, uint32_t nn, bool narrow,
+                                           uint32_t (&lamA)[4], uint32_t (&BA)[4], uint32_t &LA,
+                                           uint32_t (&lamB)[4], uint32_t (&BB)[4], uint32_t &LB)
 {
     constexpr uint32_t GLU = GL;
     const uint16_t *lgz = sm.lgz;
     const uint8_t *al2 = sm.al2;
-    uint32_t BmA[4], BmB[4], LA = 0, LB = 0;
-    for (uint32_t r = 1; r <= nr; ++r) {
+    uint32_t BmA[4], BmB[4];
+    for (uint32_t r = r0; r <= nr; ++r) {
+        if (narrow && (gw_top_set<NQ>(G, BA) || gw_top_set<NQ>(G, BB)))
+            return r;
         uint32_t pa = 0, pb = 0;
 #pragma unroll
         for (int q = 0; q < NQ; ++q) {
@@ -873,6 +901,7 @@ __device__ __forceinline__ void gw_bm2(const SM &sm, const uint16_t *szA, const 
         if (lb)
             LB = r - LB;
     }
+    return nr + 1u;
 }
 
 /* src/decode.c:98-230 after Berlekamp-Massey, for the locator lam (values,
@@ -1145,12 +1174,17 @@ __device__ bool gw_correct(const SM &sm, WT &W, const RsGenParams &P, const GMod
     /* Berlekamp-Massey, src/decode.c:49-96 (gw_bm), the slot count a
      * compile-time constant so that the slots' lookups issue together */
     uint32_t L = ne;
-    if (nq == 1u)
-        gw_bm<1>(sm, W.sz, G, nr, nn, ne, lam, B, L);
-    else if (nq == 2u)
-        gw_bm<2>(sm, W.sz, G, nr, nn, ne, lam, B, L);
-    else
-        gw_bm<4>(sm, W.sz, G, nr, nn, ne, lam, B, L);
+    if (nq == 1u) {
+        gw_bm<1>(sm, W.sz, G, ne + 1u, nr, nn, ne, false, lam, B, L);
+    } else if (nq == 2u) { /* one slot while nothing reaches the second */
+        const uint32_t r = GW_NARROW && ne < GLU ? gw_bm<1>(sm, W.sz, G, ne + 1u, nr, nn, ne, true, lam, B, L) : ne + 1u;
+        if (r <= nr)
+            gw_bm<2>(sm, W.sz, G, r, nr, nn, ne, false, lam, B, L);
+    } else { /* two slots while nothing reaches the third */
+        const uint32_t r = GW_NARROW && ne < 2u * GLU ? gw_bm<2>(sm, W.sz, G, ne + 1u, nr, nn, ne, true, lam, B, L) : ne + 1u;
+        if (r <= nr)
+            gw_bm<4>(sm, W.sz, G, r, nr, nn, ne, false, lam, B, L);
+    }
     (void)Bm;
     return gw_finish<PosT>(sm, W, P, mod, G, data, parity, pos, eras_apply, corrected, lam);
 }
@@ -1276,14 +1310,23 @@ __device__ void gw_decode_pair(const SM &sm, WT &W, uint8_t *sideS, uint16_t *si
         }
         uint32_t L = 0;
         if (dirtyA && dirtyB) {
-            if (nq == 1u)
-                gw_bm2<1>(sm, sideSz, W.sz, G, nr, P.nn, lam, Bl, lamB, BB);
-            else
-                gw_bm2<2>(sm, sideSz, W.sz, G, nr, P.nn, lam, Bl, lamB, BB);
+            uint32_t LA = 0, LB = 0;
+            if (nq == 1u) {
+                gw_bm2<1>(sm, sideSz, W.sz, G, 1u, nr, P.nn, false, lam, Bl, LA, lamB, BB, LB);
+            } else { /* one slot while nothing reaches the second */
+                const uint32_t r = GW_NARROW ? gw_bm2<1>(sm, sideSz, W.sz, G, 1u, nr, P.nn, true, lam, Bl, LA, lamB, BB, LB)
+                                             : 1u;
+                if (r <= nr)
+                    gw_bm2<2>(sm, sideSz, W.sz, G, r, nr, P.nn, false, lam, Bl, LA, lamB, BB, LB);
+            }
         } else if (nq == 1u) {
-            gw_bm<1>(sm, dirtyA ? sideSz : W.sz, G, nr, P.nn, 0u, dirtyA ? lam : lamB, dirtyA ? Bl : BB, L);
+            gw_bm<1>(sm, dirtyA ? sideSz : W.sz, G, 1u, nr, P.nn, 0u, false, dirtyA ? lam : lamB, dirtyA ? Bl : BB, L);
         } else {
-            gw_bm<2>(sm, dirtyA ? sideSz : W.sz, G, nr, P.nn, 0u, dirtyA ? lam : lamB, dirtyA ? Bl : BB, L);
+            const uint32_t r = GW_NARROW ? gw_bm<1>(sm, dirtyA ? sideSz : W.sz, G, 1u, nr, P.nn, 0u, true,
+                                                    dirtyA ? lam : lamB, dirtyA ? Bl : BB, L)
+                                           : 1u;
+            if (r <= nr)
+                gw_bm<2>(sm, dirtyA ? sideSz : W.sz, G, r, nr, P.nn, 0u, false, dirtyA ? lam : lamB, dirtyA ? Bl : BB, L);
         }
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
