@@ -40,6 +40,11 @@ reference CPU path timed on the host cores (rank 0, N=1 only).
 --backend MODULE replaces the GPU codec by MODULE.Backend (tests only: the
 gloo launcher test runs the same launcher, partition and reduction code on
 CPU with tests/bench_cpu_backend.py).
+
+POPORON_BENCH_ONE_DEVICE=1 (rehearsal only, never a scaling number): every
+rank on cuda:0 with gloo reductions on host tensors, so the N > 1 GPU path
+(launcher, per-rank ranges, kernels, per-rank reports, checksums) runs on a
+one-GPU box; the line says so under "rehearsal".
 """
 from __future__ import annotations
 
@@ -185,12 +190,22 @@ def launch_ranks(args, argv):
     return subprocess.call(cmd, env=env)
 
 
+def one_device():
+    """rehearsal: every rank on cuda:0, gloo (module docstring)"""
+    return os.environ.get("POPORON_BENCH_ONE_DEVICE") == "1"
+
+
 def dist_setup(backend_name):
     import torch
     import torch.distributed as dist
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if backend_name == "nccl" and one_device():
+        if world > 1:
+            dist.init_process_group(backend="gloo")
+        torch.cuda.set_device(0)
+        return world, rank, 0
     if world > 1:
         if backend_name == "nccl":
             torch.cuda.set_device(local)
@@ -1250,7 +1265,7 @@ def main(argv=None):
     else:
         world, rank, local = dist_setup("nccl")
         be = GpuBackend(local)
-        dev = be.dev
+        dev = "cpu" if one_device() else be.dev
     ranks = Ranks(world, dev)
 
     w = run_weak(be, ranks, args, rank, world)
@@ -1290,6 +1305,8 @@ def main(argv=None):
         "verified": w["nbad"] == 0,
         "weak_checksum": w["checksum"],
     }
+    if one_device() and not args.backend:
+        line["rehearsal"] = f"POPORON_BENCH_ONE_DEVICE: all {world} ranks on cuda:0, gloo reductions; not a scaling number"
     samples = dict(w.pop("samples"))
     if not args.no_mixed:
         mix = run_mixed(be, ranks, args, rank, world, w)
