@@ -183,7 +183,7 @@ struct _poporon_t {
     int decode_path; /* 0: by batch size, 1: split kernels (rs_fast.hip), 2: single kernel (rs_correct_k),
                       * 3: one codeword per wave (rs_wave_k) */
     bool generic;   /* served by the general-parameter kernels (rs_generic.hip) */
-    bool lfsr_nr;   /* generic byte-symbol code, num_roots < 32: batch encodes on the LFSR kernel (rsk_encode_nr) */
+    bool lfsr_nr;   /* generic code, num_roots <= 32: batch encodes on the LFSR kernel (rsk_encode_nr) */
     bool nrsplit;   /* ... and large error-mode batches decode on the split kernels (params_nrsplit) */
     int gen_path;   /* general kernels: 0 by batch size, 1 one codeword per lane (rsg_*), 2 one per wave
                        (rsgw_*); POPORON_AMD_GENERIC=lane|wave */
@@ -627,16 +627,20 @@ static bool params_supported(const poporon_t *h)
     return true;
 }
 
-/* Byte-symbol codes with fewer than 32 roots encode on the RS(255,223) LFSR
- * kernel with g'(x) = g(x) x^(32 - nr) (rsk_encode_nr, rs_kernels.hip): the
- * same steps as src/encode.c:120-143 on the first nr register bytes, zeros
- * behind them.  Like the fast path it needs a generator without zero
+/* Codes with at most 32 roots encode on the RS(255,223) LFSR kernel with
+ * g'(x) = g(x) x^(32 - nr) (rsk_encode_nr, rs_kernels.hip; 32 roots: the
+ * codes the fast path leaves to the general kernels): the same steps as
+ * src/encode.c:120-143 on the first nr register bytes, zeros behind them.
+ * Symbols of m < 8 bits too: the register bytes stay below 2^m, so the
+ * reference's feedback log[(d & nn) ^ p_0] is row (d ^ p_0) & nn, and the
+ * rows of feedback bytes >= 2^m repeat those of their low m bits
+ * (build_lfsr_rows).  Like the fast path it needs a generator without zero
  * coefficients (the reference's log-form LFSR reads a zero coefficient's log
  * literally). */
 static bool params_lfsr_nr(const poporon_t *h)
 {
     const poporon_rs_t *rs = h->rs;
-    if (rs->gf->symbol_size != 8 || rs->num_roots == 0 || rs->num_roots >= RS_NR || rs->primitive_element == 0)
+    if (rs->gf->symbol_size > 8 || rs->num_roots == 0 || rs->num_roots > RS_NR || rs->primitive_element == 0)
         return false;
     for (uint32_t i = 0; i < rs->num_roots; i++)
         if (rs->generator_polynomial[i] == rs->gf->field_size)
@@ -652,8 +656,8 @@ static bool params_lfsr_nr(const poporon_t *h)
 static bool params_nrsplit(const poporon_t *h)
 {
     const poporon_rs_t *rs = h->rs;
-    if (!params_lfsr_nr(h) || rs->num_roots < 2)
-        return false;
+    if (!params_lfsr_nr(h) || rs->gf->symbol_size != 8 || rs->num_roots < 2 || rs->num_roots >= RS_NR)
+        return false; /* GF(2^8) split kernels with npar < 32 (32 roots: the fast path's own codes) */
     const uint32_t p = rs->primitive_element;
     if (p % 3 == 0 || p % 5 == 0 || p % 17 == 0)
         return false;
@@ -661,7 +665,8 @@ static bool params_nrsplit(const poporon_t *h)
 }
 
 /* rows of g'(x) = g(x) x^(32 - nr) in the LFSR kernel's interleaved layout:
- * row byte m = fb * g_(nr-1-m) for m < nr (src/encode.c:126-140), 0 past it */
+ * row byte m = fb * g_(nr-1-m) for m < nr (src/encode.c:126-140), 0 past it;
+ * feedback byte fb selects the row of fb & nn (m < 8: params_lfsr_nr) */
 static void build_lfsr_rows(poporon_t *h)
 {
     const poporon_rs_t *rs = h->rs;
@@ -672,10 +677,11 @@ static void build_lfsr_rows(poporon_t *h)
     memset(&t, 0, sizeof(t));
     uint8_t row[32];
     for (uint32_t fb = 0; fb < 256; fb++) {
+        const uint32_t v = fb & gf->field_size;
         for (uint32_t m = 0; m < 32; m++)
-            row[m] = (fb == 0 || m >= nr)
+            row[m] = (v == 0 || m >= nr)
                          ? 0
-                         : (uint8_t)gf->log2exp[gf_mod(gf, (uint16_t)(gf->exp2log[fb] + g[nr - 1 - m]))];
+                         : (uint8_t)gf->log2exp[gf_mod(gf, (uint16_t)(gf->exp2log[v] + g[nr - 1 - m]))];
         uint32_t il[8];
         for (uint32_t k = 0; k < 8; k++)
             il[k] = (uint32_t)row[k] | ((uint32_t)row[k + 8] << 8) | ((uint32_t)row[k + 16] << 16) |
@@ -1383,7 +1389,8 @@ static bool rem_release(GpuCtx &g, hipStream_t s)
  * profiles/r06_general_lat_{wave,lane}.log) and large encode batches of
  * 255-symbol codes; the per-lane kernels large decode batches of 3- and
  * 7-symbol codes (22 us vs 32 at m = 2) and large encode batches of shorter
- * codes (one LFSR per lane: 17-217 us vs 29-274) */
+ * codes with more than 32 roots (codes with up to 32 take the RS(255,223) LFSR
+ * kernel, params_lfsr_nr) */
 static bool gen_wave(const poporon_t *h, size_t count, bool encode, size_t size)
 {
     const uint32_t nn = h->rs->gf->field_size;
@@ -1408,7 +1415,7 @@ static bool launch_encode(poporon_t *h, const uint8_t *d_data, size_t ds, uint8_
         /* one codeword: the whole workgroup (rs_enc1_k reads exp2 / log, which
          * build_decode_tables fills only for nrsplit codes) */
         HIP_OK(rsk_encode1_nr(h->gpu.tab, d_data, d_par, (uint32_t)size, h->rs->num_roots, nullptr, 0u, s));
-    } else if (h->lfsr_nr) {
+    } else if (h->lfsr_nr && !h->gen_path) { /* (POPORON_AMD_GENERIC forces the general kernels, as for decode) */
         HIP_OK(rsk_encode_nr(h->gpu.tab, d_data, ds, d_par, ps, (uint32_t)size, count, h->rs->num_roots,
                              h->gpu.num_cu, s));
     } else {

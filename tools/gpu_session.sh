@@ -58,6 +58,11 @@ for step in "$@"; do
     gwtests) run gw_tests 400 python -u -m pytest tests/test_gpu_generic_wave.py -x -q --timeout 120 --timeout-method thread ;;
     glat) run glat_wave 300 python tools/general_lat.py --calls 30 --path wave
           run glat_lane 300 python tools/general_lat.py --calls 30 --path lane ;;
+    glatauto) run glat_auto 300 python tools/general_lat.py --calls 30 ;;
+    gparity) run gparity 400 python -u -m pytest tests/test_gpu_parity.py -x -q --timeout 120 --timeout-method thread \
+                 -k "general or generic or short or lfsr" ;;
+    gbig) run gbig 400 python -u -m pytest tests/test_gpu_generic_wave.py -x -q --timeout 120 --timeout-method thread \
+                 -k "large_batch" ;;
     gwbatch) # general-parameter batch decodes: both families, then PMC of the wave family on RS(255,155)
         for prm in 8,0x11d,1,1,100 4,0x13,1,2,8 6,0x43,1,1,10 7,0x89,1,1,20; do
             for fam in wave lane; do
