@@ -579,6 +579,13 @@ static void build_generic(poporon_t *h)
     }
     for (uint32_t i = 0; i <= rs->num_roots; i++)
         t.gen[i] = (uint8_t)rs->generator_polynomial[i];
+    /* lrow: the rows of rsg_lfsr_k (rs_generic.h) */
+    for (uint32_t fb = 0; fb < 256; fb++) {
+        const uint32_t v = fb & nn;
+        for (uint32_t i = 0; i < rs->num_roots && v != 0; i++)
+            t.lrow[fb * 256 + i] = (uint8_t)gf->log2exp[gf_mod(
+                gf, (uint16_t)(gf->exp2log[v] + rs->generator_polynomial[rs->num_roots - 1 - i]))];
+    }
     /* encq: the register after each byte of the message 1, 0, 0, ... -- the
      * steps of src/encode.c:120-143 as rsg_encode_k takes them (the
      * generator's logs used as they are) */
@@ -1401,6 +1408,8 @@ static bool gen_wave(const poporon_t *h, size_t count, bool encode, size_t size)
     return count < 16384 || (encode ? nn == 255u : nn >= 15u);
 }
 
+#define GEN_LFSR_MIN 1024 /* batch size from which codes of more than 32 roots encode on rsg_lfsr_k */
+
 static bool launch_encode(poporon_t *h, const uint8_t *d_data, size_t ds, uint8_t *d_par, size_t ps, size_t size,
                           size_t count, hipStream_t s)
 {
@@ -1418,6 +1427,14 @@ static bool launch_encode(poporon_t *h, const uint8_t *d_data, size_t ds, uint8_
     } else if (h->lfsr_nr && !h->gen_path) { /* (POPORON_AMD_GENERIC forces the general kernels, as for decode) */
         HIP_OK(rsk_encode_nr(h->gpu.tab, d_data, ds, d_par, ps, (uint32_t)size, count, h->rs->num_roots,
                              h->gpu.num_cu, s));
+    } else if (h->rs->num_roots > RS_NR && !h->gen_path && count >= GEN_LFSR_MIN) {
+        /* the per-lane LFSR of 16 ceil(nr / 16) bytes (rsg_lfsr_k; smaller
+         * batches on the wave kernel, whose codeword spreads over the wave:
+         * 64 codewords 27-34 vs 34-41 us, 4,096 39-53 vs 51-53 -> 39-45,
+         * 65,536 292-524 vs 43-52 us, profiles/r06_general_lat_auto_v2.log) */
+        RsGenParams prm = h->gen;
+        prm.size = (uint32_t)size;
+        HIP_OK(rsg_lfsr_encode(h->gpu.gtab, &prm, d_data, ds, d_par, ps, count, h->gpu.num_cu, s));
     } else {
         RsGenParams prm = h->gen;
         prm.size = (uint32_t)size;

@@ -19,6 +19,10 @@ struct RsGenTables {
     /* parity of the message 1 followed by d zeros, row d (stride 256), log
      * form, 0xff: zero (the reference's LFSR, src/encode.c:120-143) */
     uint8_t encq[255 * 256];
+    /* LFSR rows of rsg_lfsr_k: row fb, register byte i (< 256) = fb' * g_(nr-1-i)
+     * for i < nr, 0 past it, fb' = fb & nn (src/encode.c:120-143's feedback
+     * of a raw byte, the reference masking it to m bits) */
+    uint8_t lrow[256 * 256];
 };
 
 struct RsGenParams {
@@ -53,6 +57,10 @@ hipError_t rsgw_check(const RsGenTables *tab, const RsGenParams *prm, const uint
                       const uint8_t *parity, size_t pstride, size_t count, uint8_t *dirty, uint16_t *syn,
                       size_t syn_stride, int num_cu, hipStream_t stream);
 
+/* batch encode on a per-lane LFSR of 16 ceil(nr / 16) register bytes (rows
+ * from tab->lrow staged in LDS): codes with more than 32 roots */
+hipError_t rsg_lfsr_encode(const RsGenTables *tab, const RsGenParams *prm, const uint8_t *data, size_t dstride,
+                           uint8_t *parity, size_t pstride, size_t count, int num_cu, hipStream_t stream);
 hipError_t rsg_encode(const RsGenTables *tab, const RsGenParams *prm, const uint8_t *data, size_t dstride,
                       uint8_t *parity, size_t pstride, size_t count, int num_cu, hipStream_t stream);
 

@@ -1683,6 +1683,145 @@ __global__ __launch_bounds__(64) void rsgw_serve_k(const RsGenTables *__restrict
 }
 
 /* ------------------------------------------------------------------------ */
+/* rsg_lfsr_k: batch encode of codes with more than 32 roots                */
+/* ------------------------------------------------------------------------ */
+
+/*
+ * src/encode.c:120-143 as a table-driven LFSR, one codeword per lane: the
+ * register is W = 16 NP bytes (byte i = byte i % 4 of dword i / 4; the
+ * parity in bytes 0 .. nr-1, highest degree first, zeros behind them: the
+ * generator g(x) x^(W - nr)), a step shifts it by one byte and XORs row fb
+ * (fb = input byte ^ register byte 0; the rows of fb >= 2^m repeat those of
+ * fb & nn, the reference's masking).  The rows are tab->lrow, staged in LDS
+ * as RP copies (gl_copies), lane l reading copy l % RP ((fb NP + piece) RP + copy
+ * 16-byte units: lanes of different copies hit different bank slots).  The
+ * per-row table keeps the reference's literal use of the generator's logs,
+ * so the result is the reference's for every generator.  Against
+ * rsgw_encode_k's table of message-position rows (size x nr products per
+ * codeword over the wave): nr / 16 16-byte reads per message byte.
+ */
+#define GL_WG 256
+#define GL_LDS (64u * 1024u) /* dynamic LDS per workgroup */
+
+template <int NP>
+constexpr uint32_t gl_copies() /* table copies in GL_LDS */
+{
+    return std::max<uint32_t>(1u, std::min<uint32_t>(16u, GL_LDS / (4096u * NP)));
+}
+
+template <int NP>
+__global__ __launch_bounds__(GL_WG) void rsg_lfsr_k(const RsGenTables *__restrict__ T, uint32_t size, uint32_t nr,
+                                                    const uint8_t *__restrict__ data, size_t dstride,
+                                                    uint8_t *__restrict__ parity, size_t pstride, size_t count)
+{
+    constexpr uint32_t RP = gl_copies<NP>();
+    extern __shared__ uint4 lrows[]; /* [(fb NP + piece) RP + copy] */
+    for (uint32_t u = threadIdx.x; u < 256u * NP; u += blockDim.x) {
+        const uint32_t fb = u / NP, j = u % NP;
+        const uint4 v = *reinterpret_cast<const uint4 *>(T->lrow + fb * 256u + 16u * j);
+        for (uint32_t r = 0; r < RP; ++r)
+            lrows[u * RP + r] = v;
+    }
+    __syncthreads();
+    const uint4 *tab = lrows + threadIdx.x % RP;
+    const uint32_t rs = NP * RP; /* units per row */
+    for (size_t cw = (size_t)blockIdx.x * blockDim.x + threadIdx.x; cw < count;
+         cw += (size_t)gridDim.x * blockDim.x) {
+        uint32_t X[4 * NP];
+#pragma unroll
+        for (int k = 0; k < 4 * NP; ++k)
+            X[k] = 0;
+        auto step = [&](uint32_t d) __attribute__((always_inline)) {
+            const uint4 *row = tab + ((X[0] ^ d) & 0xffu) * rs;
+            uint4 v[NP];
+#pragma unroll
+            for (int j = 0; j < NP; ++j)
+                v[j] = row[j * RP];
+#pragma unroll
+            for (int k = 0; k < 4 * NP - 1; ++k)
+                X[k] = __builtin_amdgcn_alignbyte(X[k + 1], X[k], 1);
+            X[4 * NP - 1] >>= 8;
+#pragma unroll
+            for (int j = 0; j < NP; ++j) {
+                X[4 * j] ^= v[j].x;
+                X[4 * j + 1] ^= v[j].y;
+                X[4 * j + 2] ^= v[j].z;
+                X[4 * j + 3] ^= v[j].w;
+            }
+        };
+        /* the message as aligned dwords that hold its bytes (no load past
+         * them), re-aligned by the row's byte offset */
+        const uint8_t *p = data + cw * dstride;
+        const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+        const uint32_t *w = reinterpret_cast<const uint32_t *>(a & ~uintptr_t(3));
+        const uint32_t sh = (uint32_t)(a & 3u), nd = (sh + size + 3u) >> 2;
+        uint32_t cur = w[0];
+        uint32_t q = 0, i = 0;
+        for (; i + 4u <= size; i += 4u, ++q) {
+            const uint32_t nxt = q + 1u < nd ? w[q + 1u] : 0u;
+            const uint32_t m = __builtin_amdgcn_alignbyte(nxt, cur, sh);
+            step(m);
+            step(m >> 8);
+            step(m >> 16);
+            step(m >> 24);
+            cur = nxt;
+        }
+        if (i < size) {
+            const uint32_t nxt = q + 1u < nd ? w[q + 1u] : 0u;
+            const uint32_t m = __builtin_amdgcn_alignbyte(nxt, cur, sh);
+            for (uint32_t b = 0; b < size - i; ++b)
+                step(m >> (8u * b));
+        }
+        /* the first nr register bytes: whole dwords as unaligned dword
+         * stores, the last 0..3 bytes one by one */
+        typedef __attribute__((address_space(1))) uint32_t gu32s __attribute__((aligned(1)));
+        uint8_t *o = parity + cw * pstride;
+        const uint32_t nw = nr >> 2, nt = nr & 3u;
+        uint32_t tail = 0;
+#pragma unroll
+        for (int k = 0; k < 4 * NP; ++k) {
+            if ((uint32_t)k < nw)
+                *(gu32s *)(uintptr_t)(o + 4 * k) = X[k];
+            tail = (uint32_t)k == nw ? X[k] : tail;
+        }
+        for (uint32_t b = 0; b < nt; ++b)
+            o[4u * nw + b] = (uint8_t)(tail >> (8u * b));
+    }
+}
+
+template <int NP>
+static void rsg_lfsr_launch(const RsGenTables *tab, const RsGenParams &P, const uint8_t *data, size_t dstride,
+                            uint8_t *parity, size_t pstride, size_t count, int num_cu, hipStream_t stream,
+                            uint32_t np)
+{
+    if constexpr (NP <= 16) {
+        if (np != (uint32_t)NP) {
+            rsg_lfsr_launch<NP + 1>(tab, P, data, dstride, parity, pstride, count, num_cu, stream, np);
+            return;
+        }
+        const size_t lds = (size_t)4096u * NP * gl_copies<NP>();
+        const size_t need = (count + GL_WG - 1) / GL_WG;
+        const size_t cap = (size_t)(num_cu > 0 ? num_cu : 256) * 2u;
+        const dim3 grid((uint32_t)std::max<size_t>(1, std::min(need, cap)));
+        RS_LAUNCH(rsg_lfsr_k<NP>, grid, dim3(GL_WG), lds, stream, tab, P.size, P.nroots, data, dstride, parity,
+                  pstride, count);
+    }
+}
+
+extern "C" hipError_t rsg_lfsr_encode(const RsGenTables *tab, const RsGenParams *prm, const uint8_t *data,
+                                      size_t dstride, uint8_t *parity, size_t pstride, size_t count, int num_cu,
+                                      hipStream_t stream)
+{
+    if (count == 0)
+        return hipSuccess;
+    const uint32_t np = (prm->nroots + 15u) / 16u;
+    if (np < 1u || np > 16u)
+        return hipErrorInvalidValue;
+    rsg_lfsr_launch<1>(tab, *prm, data, dstride, parity, pstride, count, num_cu, stream, np);
+    return hipGetLastError();
+}
+
+/* ------------------------------------------------------------------------ */
 /* launchers                                                                */
 /* ------------------------------------------------------------------------ */
 
