@@ -1016,12 +1016,14 @@ def general_params(be, n=1 << 20, reps=5, params=(8, 0x11D, 1, 1, 16), nerr=8):
 def general_wave(be, sets=((8, 0x11D, 1, 1, 100), (4, 0x13, 1, 2, 8)), n=1 << 16, calls=200, reps=3):
     """SURVEY 8(f) row 1 beyond the fewer-roots codes: parameter sets of the
     reference's own tests that run on the general kernels (rs_generic.hip) --
-    RS(255,155) (100 roots: one codeword per wave, rsgw_*) and RS(15,7) over
-    GF(16) with prim 2 (single calls on rsgw_*, its large batches one
-    codeword per lane, rsg_*): single-call encode / decode latency through
-    ctypes (t errors) and a device batch of n codewords with t errors each
-    (wall, stream-synchronised, median of reps).  Every 256th batch codeword
-    and every single call are compared with the oracle restatement."""
+    RS(255,155) (100 roots: decode one codeword per wave, two per pass,
+    rsgw_*; batch encode on the per-lane LFSR rsg_lfsr_k) and RS(15,7) over
+    GF(16) with prim 2 (decode sixteen codewords per wave, 4-lane groups;
+    batch encode on the RS(255,223) LFSR kernel): single-call encode / decode
+    latency through ctypes (t errors), a device batch decode of n codewords
+    with t errors each (wall, stream-synchronised, and device events; median
+    of reps) and a device batch encode (device events).  Every 256th batch
+    codeword and every single call are compared with the oracle restatement."""
     import numpy as np
 
     from oracle import Oracle
@@ -1079,6 +1081,21 @@ def general_wave(be, sets=((8, 0x11D, 1, 1, 100), (4, 0x13, 1, 2, 8)), n=1 << 16
             be.sync()
             tk.append(e0.elapsed_time(e1) * 1e-3)
         got, gok, gcor = buf.cpu().numpy(), ok.cpu().numpy(), cor.cpu().numpy()
+        # device batch encode of the same messages into rows [data | parity]
+        erow = torch.from_numpy(np.concatenate([data, np.zeros_like(par)], 1)).to(be.dev)
+        eb = erow.data_ptr()
+        te_dev = []
+        for r in range(reps + 1):
+            be.sync()
+            torch.cuda._sleep(200000)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            h.encode_batch_device(eb, nn, eb + k, nn, k, n, s)
+            e1.record()
+            be.sync()
+            if r:
+                te_dev.append(e0.elapsed_time(e1) * 1e-3)
+        mism += int((erow.cpu().numpy()[:, k:] != par).any(1).sum())
         idx = np.arange(0, n, 256)
         ook, ocor, od, op = o.decode_batch(bad[idx, :k], bad[idx, k:])
         mism += int(((ook != gok[idx]) | (ocor != gcor[idx]) | (od != got[idx, :k]).any(1) |
@@ -1090,11 +1107,15 @@ def general_wave(be, sets=((8, 0x11D, 1, 1, 100), (4, 0x13, 1, 2, 8)), n=1 << 16
             "single_encode_us": round(te * 1e6, 1), "single_decode_us": round(td * 1e6, 1),
             "batch_codewords": n, "batch_decode_cw_per_s": round(n / d, 1), "batch_decode_ms": round(d * 1e3, 4),
             "batch_decode_device_cw_per_s": round(n / dk, 1), "batch_decode_device_ms": round(dk * 1e3, 4),
+            "batch_encode_device_cw_per_s": round(n / float(np.median(te_dev)), 1),
+            "batch_encode_device_ms": round(float(np.median(te_dev)) * 1e3, 4),
             "errors_per_codeword": t, "mismatches": mism}
         h.close()
     out["note"] = ("single calls: poporon_encode / poporon_decode through ctypes (one wave, coherent host memory); "
                    "batch: poporon_decode_batch_device, wall time of the Python call (batch_decode_*) and device "
-                   "time between HIP events on its stream (batch_decode_device_*); checked against oracle/rs_oracle.c")
+                   "time between HIP events on its stream (batch_decode_device_*); poporon_encode_batch_device of the "
+                   "same messages (batch_encode_device_*, its parity equal to the host batch's, which is sampled "
+                   "against the oracle); checked against oracle/rs_oracle.c")
     out["verified"] = all(v["mismatches"] == 0 for kk, v in out.items() if isinstance(v, dict))
     return out
 
