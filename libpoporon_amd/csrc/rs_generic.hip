@@ -1755,7 +1755,7 @@ __global__ __launch_bounds__(GL_WG) void rsg_lfsr_k(const RsGenTables *__restric
         const uintptr_t a = reinterpret_cast<uintptr_t>(p);
         const uint32_t *w = reinterpret_cast<const uint32_t *>(a & ~uintptr_t(3));
         const uint32_t sh = (uint32_t)(a & 3u), nd = (sh + size + 3u) >> 2;
-        uint32_t cur = w[0];
+        uint32_t cur = size ? w[0] : 0u; /* size 0: zero parity, nothing read */
         uint32_t q = 0, i = 0;
         for (; i + 4u <= size; i += 4u, ++q) {
             const uint32_t nxt = q + 1u < nd ? w[q + 1u] : 0u;
