@@ -72,6 +72,12 @@ for step in "$@"; do
         POPORON_AMD_GENERIC=wave run gwb_pmc 200 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_WAVE_CYCLES \
             SQ_BUSY_CYCLES SQ_WAIT_INST_LDS SQ_ACTIVE_INST_VALU SQ_WAIT_ANY GRBM_GUI_ACTIVE -d gpurun_out/gwb_pmc \
             -o pmc --output-format csv -- python3 tools/gw_batch.py --params 8,0x11d,1,1,100 --reps 3 ;;
+    gwconf) # LDS bank conflicts of the general wave decode (RS(255,155)), then of RS(15,7)
+        for prm in 8,0x11d,1,1,100 4,0x13,1,2,8; do
+            POPORON_AMD_GENERIC=wave run gwconf_${prm//,/_} 200 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE \
+                SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_INSTS_VALU SQ_BUSY_CYCLES GRBM_GUI_ACTIVE \
+                -d gpurun_out/gwconf_${prm//,/_} -o pmc --output-format csv -- python3 tools/gw_batch.py --params $prm --reps 3
+        done ;;
     gwab) # general batch decodes on each build in build/*.so (RS(255,155), RS(127,107), RS(15,7)), alternated twice
         for pass in 1 2; do
             for so in build/gw[A-Z]*.so; do
