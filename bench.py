@@ -1013,7 +1013,7 @@ def general_params(be, n=1 << 20, reps=5, params=(8, 0x11D, 1, 1, 16), nerr=8):
             "sample": {"checker": "port: oracle/rs_oracle.c (pinned)", "n": int(len(idx)), "mismatches": mism}}
 
 
-def general_wave(be, sets=((8, 0x11D, 1, 1, 100), (4, 0x13, 1, 2, 8)), n=1 << 16, calls=200, reps=3):
+def general_wave(be, sets=((8, 0x11D, 1, 1, 100), (4, 0x13, 1, 2, 8)), n=1 << 16, calls=200, reps=7):
     """SURVEY 8(f) row 1 beyond the fewer-roots codes: parameter sets of the
     reference's own tests that run on the general kernels (rs_generic.hip) --
     RS(255,155) (100 roots: decode one codeword per wave, two per pass,
